@@ -1,0 +1,251 @@
+/*
+ * sightpy_rt.h -- C ABI of the MI355X (gfx950) ray-trace backend, libsightpy_hip.so.
+ *
+ * This is the drop-in boundary for the hot path of lmondada/Python-Raytracer ("sightpy").
+ * The reference is pure Python/numpy with no FFI; each entry point below replaces one Python
+ * interface of the reference and is what a ctypes binding of that interface calls
+ * (the binding is python-raytracer_amd/sightpy/_native.py):
+ *
+ *   srt_render             <- Scene.render            sightpy/scene.py:71-140
+ *                             (camera.get_ray per sample, get_raycolor recursion, spp average,
+ *                              sRGB_linear_to_sRGB + clip + uint8 resolve)
+ *   srt_trace              <- get_raycolor(ray, scene) sightpy/ray.py:122-148
+ *   srt_nearest            <- get_distances / the nearest-hit reduction
+ *                                                     sightpy/ray.py:124-132, 151-163
+ *   srt_intersect_collider <- Collider.intersect(O, D) sightpy/geometry/collider.py:12-14
+ *                             (sphere.py:26-52, plane.py:57-90, cuboid.py:105-140,
+ *                              triangle.py:36-66)
+ *   srt_primary_rays       <- Camera.get_ray(n)       sightpy/camera.py:51-85
+ *   srt_upload_scene       <- (scene lowering; the reference deep-copies the Scene per task,
+ *                              scene.py:85)
+ *
+ * Conventions
+ *   - Every entry point returns 0 on success or a negative SRT_ERR_* code; the message of the
+ *     last failure on the calling thread is srt_last_error().  No C++ exception crosses the ABI.
+ *   - Array arguments are plain pointers + sizes.  Vectors are planar [3][n] float64 (the
+ *     reference's vec3.to_array() layout).  A pointer may address host memory or device memory
+ *     of the context's GPU (copies use hipMemcpyDefault); host memory is borrowed for the call.
+ *   - All arithmetic is IEEE float64 (complex128 for the index of refraction), evaluated in the
+ *     reference's operation order with FP contraction disabled.
+ *   - One context = one GPU; a context must be used by one host thread at a time.
+ */
+#ifndef SIGHTPY_RT_H
+#define SIGHTPY_RT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRT_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------------------------ */
+#define SRT_OK 0
+#define SRT_ERR_ARG -1      /* bad argument / unsupported scene feature */
+#define SRT_ERR_HIP -2      /* HIP runtime failure (message has the hipError string) */
+#define SRT_ERR_NOSCENE -3  /* render/trace before srt_upload_scene */
+#define SRT_ERR_MEMORY -4   /* queue / framebuffer allocation failed */
+#define SRT_ERR_INDEX -5    /* a table index left its array (the reference raises IndexError) */
+#define SRT_ERR_DEPTH -6    /* rays still alive after the depth cap */
+
+/* ---- scene tables --------------------------------------------------------------------- */
+enum { SRT_SPHERE = 0, SRT_PLANE = 1, SRT_CUBOID = 2, SRT_TRIANGLE = 3 };
+enum {
+    SRT_GLOSSY = 0,
+    SRT_REFRACTIVE = 1,
+    SRT_THINFILM = 2,
+    SRT_DIFFUSE = 3,
+    SRT_EMISSIVE = 4,
+    SRT_SKY = 5
+};
+/* collider flags */
+#define SRT_CF_SHADOW 1u   /* member of scene.shadowed_collider_list */
+#define SRT_CF_MC 2u       /* primitive.mc: Monte-Carlo refraction pick */
+#define SRT_CF_UV_CROSS 4u /* Cuboid/SkyBox primitive: uv /= (4, 3) */
+/* material flags */
+#define SRT_MF_ROUGH 1u    /* Glossy: roughness != 0 (specular lobe on) */
+#define SRT_MF_LIGHTMAP 2u /* SkyBox: light_intensity != 0 (lightmap on non-primary rays) */
+#define SRT_MF_NOISE 4u    /* ThinFilm: noise != 0 (thickness jitter from noise texture) */
+
+#define SRT_COLLIDER_PARAMS 48
+#define SRT_MATERIAL_PARAMS 16
+
+/*
+ * Collider parameter layout (p[]), all float64, host-precomputed exactly as the reference:
+ *   SPHERE   0-2 center, 3 radius, 4 1.0/radius, 5 center.square_length(), 6 radius*radius
+ *   PLANE    0-2 center, 3-5 normal, 6-8 u_axis, 9-11 v_axis, 12 w, 13 h, 14-15 uv_shift,
+ *            16-24 inverse_basis_matrix (row-major)
+ *   CUBOID   0-2 center, 3-11 basis_matrix (row-major), 12-14 lb_local_basis,
+ *            15-17 rt_local_basis, 18-20 ax_w, 21-23 ax_h, 24-26 ax_l, 27 width, 28 height,
+ *            29 length, 30-38 inverse_basis_matrix (row-major), 39-41 (1/width,1/height,1/length)
+ *   TRIANGLE 0-2 centroid, 3-5 normal, 6-8 p1, 9-11 p2, 12-14 p3, 15-17 n31, 18-20 n12,
+ *            21-23 n23
+ */
+typedef struct srt_collider {
+    int32_t type;          /* SRT_SPHERE .. */
+    int32_t material;      /* index into the material table */
+    int32_t max_ray_depth; /* primitive.max_ray_depth */
+    uint32_t flags;        /* SRT_CF_* */
+    int32_t primitive;     /* index of the owning primitive (diagnostics) */
+    int32_t reserved[3];
+    double p[SRT_COLLIDER_PARAMS];
+} srt_collider;
+
+/*
+ * Material parameter layout (p[]):
+ *   GLOSSY     0-2 solid diffuse colour * diff_coeff (tex < 0), 3 diff_coeff, 4 a = 2/r^2 - 2,
+ *              5 a + 2.0, 6 2.0*pi, 7 spec_coeff, 8-10 F0 of the reflection term (scene.n vs n)
+ *              (the specular F0 depends on the ray's medium: srt_scene_desc.glossy_f0)
+ *   REFRACTIVE (index of refraction = media[medium])
+ *   THINFILM   0 thickness, 1 noise factor
+ *   DIFFUSE    0-2 solid colour, 3 ambient_weight, 4 1 - ambient_weight
+ *   EMISSIVE   0-2 solid colour
+ *   SKY        0 light_intensity
+ */
+typedef struct srt_material {
+    int32_t type;      /* SRT_GLOSSY .. */
+    int32_t tex;       /* colour texture (GLOSSY/DIFFUSE/EMISSIVE/SKY), -1 = solid colour */
+    int32_t tex_aux0;  /* THINFILM: reflectance table; SKY: lightmap */
+    int32_t tex_aux1;  /* THINFILM: thickness noise */
+    int32_t normalmap; /* normal-map texture, -1 = none */
+    int32_t medium;    /* REFRACTIVE: media[] row holding its n */
+    uint32_t flags;    /* SRT_MF_* */
+    int32_t ival;      /* DIFFUSE: diffuse_rays */
+    double p[SRT_MATERIAL_PARAMS];
+} srt_material;
+
+/*
+ * A texture is a uint8 image in the shared texel pool plus a 256-entry float64 table: a texel
+ * byte b reads as lut[b].  lut = sRGB_to_sRGB_linear(b/256) for linear-sRGB images, b/256 for
+ * raw ones, which reproduces the reference's float arrays bit for bit.  The lookup index is
+ *   row = -(trunc(v*idx_h*repeat) mod idx_h), col = trunc(u*idx_w*repeat) mod idx_w
+ * (texture.py:32-39), with numpy negative-index wrap against `height`.
+ */
+typedef struct srt_texture {
+    int64_t offset;   /* byte offset of texel (0,0) in the pool */
+    int32_t height;   /* rows of the stored image */
+    int32_t width;    /* columns */
+    int32_t channels; /* bytes per texel (>= 3, or 1..4 with channel0) */
+    int32_t channel0; /* first channel read */
+    int32_t idx_h;    /* shape used by the index arithmetic (== height except the lightmap) */
+    int32_t idx_w;
+    double repeat;
+    double lut[256];
+} srt_texture;
+
+enum { SRT_LIGHT_DIRECTIONAL = 0, SRT_LIGHT_POINT = 1 };
+typedef struct srt_light {
+    int32_t type;
+    int32_t reserved;
+    double dir[3]; /* DirectionalLight.Ldir (normalised by Scene.add_DirectionalLight) */
+    double color[3];
+    double pos[3]; /* PointLight.pos */
+} srt_light;
+
+typedef struct srt_scene_desc {
+    int32_t n_colliders;
+    int32_t n_materials;
+    int32_t n_textures;
+    int32_t n_lights;
+    int32_t n_media;      /* rows of media[]; row 0 is scene.n */
+    int32_t n_importance; /* scene.importance_sampled_list */
+    const srt_collider* colliders; /* scene.collider_list order */
+    const srt_material* materials;
+    const srt_texture* textures;
+    const uint8_t* texels;
+    int64_t texel_bytes;
+    const srt_light* lights;
+    const double* media;       /* [n_media][6]: Re n (3), Im n (3) */
+    const double* glossy_f0;   /* [n_materials][n_media][3]: |(n_ray-n)/(n_ray+n)|^2 */
+    const double* light_local; /* [n_lights][n_colliders][3]: Ldir.matmul(basis) (cuboids) */
+    const double* importance;  /* [n_importance][4]: center xyz, bounded_sphere_radius */
+    double ambient[3];         /* scene.ambient_color */
+    int32_t max_ray_depth;     /* max over colliders (depth cap = this + 1, +2 with Diffuse) */
+    int32_t has_diffuse;
+} srt_scene_desc;
+
+/* ---- camera / render ------------------------------------------------------------------ */
+typedef struct srt_camera {
+    int32_t width;  /* screen_width */
+    int32_t height; /* screen_height */
+    const double* xs; /* [width]  np.linspace(-cw/2, cw/2, width) */
+    const double* ys; /* [height] np.linspace(ch/2, -ch/2, height) */
+    double look_from[3];
+    double right[3];  /* cameraRight */
+    double up[3];     /* cameraUp */
+    double fwd_fd[3]; /* cameraFwd * focal_distance */
+    double cam_width;
+    double cam_height;
+    double lens_radius;
+    double focal_distance;
+} srt_camera;
+
+typedef struct srt_render_args {
+    int32_t spp;          /* samples traced by this call */
+    int32_t sample_base;  /* global index of the first sample (RNG key) */
+    int32_t n_rows;       /* rows rendered by this call (a shard of the image) */
+    int32_t batch_spp;    /* samples per device pass (0 = fit to the HBM budget) */
+    const int32_t* rows;  /* [n_rows] global row index of each local row; NULL = 0..n_rows-1 */
+    const double* jitter; /* [spp][4][n_rows*width] uniforms (x-jitter, y-jitter, r, phi) in
+                             numpy's draw order, or NULL = device Philox keyed by (seed, pixel,
+                             sample) */
+    uint64_t seed;        /* device RNG key (jitter when jitter == NULL, Monte-Carlo shading) */
+    double* out_rgb;      /* [3][n_rows*width] linear RGB averaged over spp, or NULL */
+    uint8_t* out_srgb8;   /* [n_rows*width][3] resolved image, or NULL */
+    int32_t* out_hit_id;  /* [spp][n_rows*width] primary nearest collider (-1 miss), or NULL */
+} srt_render_args;
+
+#define SRT_MAX_DEPTHS 64
+typedef struct srt_stats {
+    int64_t rays_per_depth[SRT_MAX_DEPTHS]; /* rays entering each trace depth (all passes) */
+    int64_t total_rays;                     /* sum of rays_per_depth */
+    int64_t shadow_rays;
+    int32_t n_depths;
+    int32_t passes;
+    double ms_wall;          /* host wall time inside the call */
+    double ms_device;        /* first launch -> last kernel end, HIP events */
+    double ms_trace_kernels; /* sum of trace-kernel durations, HIP events */
+    double ms_primary_kernel;
+    int64_t retries;         /* passes re-run after a queue overflow */
+} srt_stats;
+
+typedef struct srt_trace_args {
+    int64_t n;
+    const double* origin; /* [3][n] */
+    const double* dir;    /* [3][n] */
+    const int32_t* medium; /* [n] rows of media[] (ray.n), or NULL = all scene.n */
+    int32_t depth;        /* Ray.depth (a batch scalar in the reference) */
+    int32_t diffuse_reflections;
+    uint64_t seed;
+    double* out_rgb;      /* [3][n] colour of each ray */
+} srt_trace_args;
+
+typedef struct srt_ctx srt_ctx;
+
+int srt_abi_version(void);
+int srt_device_count(int* count);
+int srt_create(int device, srt_ctx** out);
+int srt_destroy(srt_ctx* ctx);
+/* options: "queue_bytes" (HBM budget for ray queues), "block_size" (reserved) */
+int srt_set_option(srt_ctx* ctx, const char* key, int64_t value);
+int srt_upload_scene(srt_ctx* ctx, const srt_scene_desc* scene);
+int srt_render(srt_ctx* ctx, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);
+int srt_trace(srt_ctx* ctx, const srt_trace_args* args, srt_stats* stats);
+int srt_nearest(srt_ctx* ctx, const double* origin, const double* dir, int64_t n, double* t,
+                int32_t* id, double* orient);
+int srt_intersect_collider(srt_ctx* ctx, const srt_collider* collider, const double* origin,
+                           const double* dir, int64_t n, double* out /* [2][n] */);
+int srt_primary_rays(srt_ctx* ctx, const srt_camera* cam, const double* jitter /* [4][n] */,
+                     double* origin /* [3][n] */, double* dir /* [3][n] */);
+/* Device memory helpers for callers that keep inputs resident in HBM (bench, multi-GPU). */
+int srt_device_alloc(srt_ctx* ctx, int64_t bytes, void** out);
+int srt_device_free(srt_ctx* ctx, void* ptr);
+int srt_memcpy(srt_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int srt_synchronize(srt_ctx* ctx);
+const char* srt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIGHTPY_RT_H */

@@ -1,0 +1,802 @@
+// rt_device.h -- per-ray math of the sightpy hot path, shared by the gfx950 kernels
+// (rt_kernels.hip) and the sequential host check harness (rt_hostcheck.cpp, tests only).
+//
+// Every function restates a numpy expression of the reference (lmondada/Python-Raytracer,
+// cited file:line) for ONE ray, in the reference's evaluation order: numpy evaluates
+// `a + b + c` as ((a+b)+c) and `x * y / z` as ((x*y)/z), vec3.dot is ((x*x'+y*y')+z*z'),
+// and vec3.matmul goes through OpenBLAS dgemm, i.e. fma(B[i][2], z, fma(B[i][1], y, B[i][0]*x)).
+// The file must be compiled with -ffp-contract=off so that only the explicit fma() calls fuse.
+// With that, + - * / sqrt are IEEE-exact on both sides, so intersections, normals, directions
+// and texel indices match the numpy reference bit for bit; transcendental functions (pow, exp,
+// atan2, asin, sin, cos, hypot) differ from numpy's SIMD versions by ~1 ulp.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/sightpy_rt.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RT_HD __host__ __device__ __forceinline__
+#define RT_HDM __host__ __device__ __forceinline__
+#else
+#define RT_HD static inline
+#define RT_HDM inline
+#endif
+
+namespace rt {
+
+// constants (reference utils/constants.py:1-4)
+constexpr double FARAWAY = 1.0e39;
+constexpr double SKYBOX_DISTANCE = 1.0e6;
+constexpr double PI = 3.141592653589793;      // np.pi
+constexpr double TWO_PI = 6.283185307179586;  // 2 * np.pi
+constexpr double HALF_PI = 1.5707963267948966;  // np.pi / 2
+constexpr double NUDGE = 0.000001;              // glossy.py:35 etc.
+
+// error bits raised by a kernel (folded into SRT_ERR_* by the host)
+constexpr uint32_t ERR_INDEX = 1u;      // texture/table index outside the array (IndexError)
+constexpr uint32_t ERR_UNSUPPORTED = 2u;  // uv of a Triangle (undefined in the reference)
+
+struct d3 {
+    double x, y, z;
+};
+
+RT_HD d3 mk(double x, double y, double z) { return d3{x, y, z}; }
+RT_HD d3 ld3(const double* p) { return d3{p[0], p[1], p[2]}; }
+RT_HD d3 add(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_HD d3 sub(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_HD d3 mul(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RT_HD d3 mul(d3 a, double s) { return d3{a.x * s, a.y * s, a.z * s}; }
+RT_HD d3 rsub(double s, d3 a) { return d3{s - a.x, s - a.y, s - a.z}; }
+RT_HD d3 divs(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
+RT_HD double dot(d3 a, d3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+RT_HD bool is_zero(d3 a) { return a.x == 0.0 && a.y == 0.0 && a.z == 0.0; }
+
+// vec3.normalize (vector3.py:158-160): v * (1.0 / where(|v| == 0, 1, |v|))
+RT_HD d3 normalize(d3 v) {
+    double mag = sqrt(dot(v, v));
+    double inv = 1.0 / (mag == 0.0 ? 1.0 : mag);
+    return mul(v, inv);
+}
+
+// vec3.matmul on arrays = np.tensordot(B, v) -> OpenBLAS dgemm: one fma chain per row
+// (vector3.py:93-97; order verified bit-exact against OpenBLAS 0.3.29)
+RT_HD d3 matmul_rows(const double* B, d3 v) {
+    return d3{fma(B[2], v.z, fma(B[1], v.y, B[0] * v.x)),
+              fma(B[5], v.z, fma(B[4], v.y, B[3] * v.x)),
+              fma(B[8], v.z, fma(B[7], v.y, B[6] * v.x))};
+}
+
+// np.minimum / np.maximum: NaN-propagating, first operand wins on NaN
+RT_HD double np_min(double a, double b) { return (a < b || a != a) ? a : b; }
+RT_HD double np_max(double a, double b) { return (a > b || a != a) ? a : b; }
+RT_HD double np_clip(double x, double lo, double hi) { return np_min(np_max(x, lo), hi); }
+// np.sign
+RT_HD double np_sign(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x)); }
+
+// ndarray.astype(int) of float64: truncation; out-of-range / NaN give INT64_MIN (x86 cvttsd2si)
+RT_HD int64_t np_trunc(double x) {
+    return (x > -9.2e18 && x < 9.2e18) ? (int64_t)x : (int64_t)(-9223372036854775807LL - 1);
+}
+// Python/numpy integer floor-mod (result has the sign of m)
+RT_HD int64_t py_mod(int64_t a, int64_t m) {
+    int64_t r = a % m;
+    return (r != 0 && (r < 0) != (m < 0)) ? r + m : r;
+}
+
+// ---- complex128 (numpy semantics) ---------------------------------------------------------
+struct cplx {
+    double re, im;
+};
+RT_HD cplx cadd(cplx a, cplx b) { return cplx{a.re + b.re, a.im + b.im}; }
+RT_HD cplx csub(cplx a, cplx b) { return cplx{a.re - b.re, a.im - b.im}; }
+RT_HD cplx cmul(cplx a, cplx b) { return cplx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+// complex * real array (numpy promotes the real operand to (x, 0))
+RT_HD cplx cmulr(cplx a, double x) { return cplx{a.re * x - a.im * 0.0, a.re * 0.0 + a.im * x}; }
+// numpy complex division (Smith's algorithm, umath loops)
+RT_HD cplx cdiv(cplx a, cplx b) {
+    double abr = fabs(b.re), abi = fabs(b.im);
+    if (abr >= abi) {
+        if (abr == 0.0 && abi == 0.0) return cplx{a.re / abr, a.im / abr};
+        double rat = b.im / b.re;
+        double scl = 1.0 / (b.re + b.im * rat);
+        return cplx{(a.re + a.im * rat) * scl, (a.im - a.re * rat) * scl};
+    }
+    double rat = b.re / b.im;
+    double scl = 1.0 / (b.im + b.re * rat);
+    return cplx{(a.re * rat + a.im) * scl, (a.im * rat - a.re) * scl};
+}
+RT_HD double cabs(cplx a) { return hypot(a.re, a.im); }
+// principal square root (glibc csqrt arrangement)
+RT_HD cplx csqrt_np(cplx z) {
+    double x = z.re, y = z.im;
+    if (x == 0.0 && y == 0.0) return cplx{0.0, y};
+    double d = hypot(x, y);
+    double r, s;
+    if (x > 0.0) {
+        r = sqrt(0.5 * (d + x));
+        s = 0.5 * (y / r);
+    } else {
+        s = sqrt(0.5 * (d - x));
+        r = fabs(0.5 * (y / s));
+    }
+    return cplx{r, copysign(s, y)};
+}
+
+// ---- scene view ---------------------------------------------------------------------------
+struct SceneView {
+    const srt_collider* col;
+    const srt_material* mat;
+    const srt_texture* tex;
+    const uint8_t* texels;
+    const srt_light* lights;
+    const double* media;
+    const double* glossy_f0;
+    const double* light_local;
+    const double* importance;
+    int ncol, nmat, ntex, nlights, nmedia, nimp;
+    int nshadow;  // colliders flagged SRT_CF_SHADOW
+    double ambient[3];
+};
+
+// ---- ray/primitive intersection (returns distance; orientation through `o`) -----------------
+// sphere.py:26-52
+RT_HD double sphere_hit(const double* p, d3 O, d3 D, double& o) {
+    d3 C = ld3(p);
+    double b = 2.0 * dot(D, sub(O, C));
+    double c = ((p[5] + dot(O, O)) - 2.0 * dot(C, O)) - p[6];
+    double disc = b * b - 4.0 * c;
+    double sq = sqrt(np_max(0.0, disc));
+    double h0 = (-b - sq) / 2.0;
+    double h1 = (-b + sq) / 2.0;
+    double h = (h0 > 0.0 && h0 < h1) ? h0 : h1;
+    d3 M = add(O, mul(D, h));
+    double nd = dot(mul(sub(M, C), p[4]), D);
+    bool ok = disc > 0.0 && h > 0.0;
+    if (ok && nd > 0.0) { o = -1.0; return h; }
+    if (ok && nd < 0.0) { o = 1.0; return h; }
+    o = FARAWAY;
+    return FARAWAY;
+}
+
+// plane.py:57-90 (rectangle: |u| <= w, |v| <= h in the plane basis)
+RT_HD double plane_hit(const double* p, d3 O, d3 D, double& o) {
+    d3 N = ld3(p + 3);
+    double nd = dot(N, D);
+    nd = (nd == 0.0) ? nd + 0.0001 : nd;
+    double nco = dot(N, sub(ld3(p), O));
+    d3 d = d3{(D.x * nco) / nd, (D.y * nco) / nd, (D.z * nco) / nd};
+    d3 M = add(O, d);
+    double dis = sqrt(dot(d, d));
+    d3 MC = sub(M, ld3(p));
+    double u = dot(ld3(p + 6), MC);
+    double v = dot(ld3(p + 9), MC);
+    if (fabs(u) <= p[12] && fabs(v) <= p[13] && nco * nd > 0.0) {
+        o = (nd < 0.0) ? 1.0 : -1.0;
+        return dis;
+    }
+    o = FARAWAY;
+    return FARAWAY;
+}
+
+// cuboid.py:105-140 (slab test in the local basis).  `Dl` is D.matmul(basis); it is passed in
+// because for shadow rays D is a scalar vec3 whose matmul goes through BLAS gemv on the host.
+RT_HD double cuboid_hit_local(const double* p, d3 O, d3 Dl, double& o) {
+    d3 Ol = matmul_rows(p + 3, O);
+    d3 f = d3{1.0 / Dl.x, 1.0 / Dl.y, 1.0 / Dl.z};
+    double t1 = (p[12] - Ol.x) * f.x, t2 = (p[15] - Ol.x) * f.x;
+    double t3 = (p[13] - Ol.y) * f.y, t4 = (p[16] - Ol.y) * f.y;
+    double t5 = (p[14] - Ol.z) * f.z, t6 = (p[17] - Ol.z) * f.z;
+    double tmin = np_max(np_max(np_min(t1, t2), np_min(t3, t4)), np_min(t5, t6));
+    double tmax = np_min(np_min(np_max(t1, t2), np_max(t3, t4)), np_max(t5, t6));
+    if (tmax < 0.0 || tmin > tmax) { o = FARAWAY; return FARAWAY; }
+    if (tmin < 0.0) { o = -1.0; return tmax; }
+    o = 1.0;
+    return tmin;
+}
+RT_HD double cuboid_hit(const double* p, d3 O, d3 D, double& o) {
+    return cuboid_hit_local(p, O, matmul_rows(p + 3, D), o);
+}
+
+// triangle.py:36-66 (plane through the centroid + edge half-spaces)
+RT_HD double triangle_hit(const double* p, d3 O, d3 D, double& o) {
+    d3 N = ld3(p + 3);
+    double nd = dot(N, D);
+    nd = (nd == 0.0) ? nd + 0.0001 : nd;
+    double nco = dot(N, sub(ld3(p), O));
+    d3 d = d3{(D.x * nco) / nd, (D.y * nco) / nd, (D.z * nco) / nd};
+    d3 M = add(O, d);
+    double dis = sqrt(dot(d, d));
+    bool inside = dot(ld3(p + 15), sub(M, ld3(p + 6))) >= 0.0 &&
+                  dot(ld3(p + 18), sub(M, ld3(p + 9))) >= 0.0 &&
+                  dot(ld3(p + 21), sub(M, ld3(p + 12))) >= 0.0 && nco * nd > 0.0;
+    if (inside) {
+        o = (nd < 0.0) ? 1.0 : -1.0;
+        return dis;
+    }
+    o = FARAWAY;
+    return FARAWAY;
+}
+
+RT_HD double collider_hit(const srt_collider& c, d3 O, d3 D, double& o) {
+    switch (c.type) {
+        case SRT_SPHERE: return sphere_hit(c.p, O, D, o);
+        case SRT_PLANE: return plane_hit(c.p, O, D, o);
+        case SRT_CUBOID: return cuboid_hit(c.p, O, D, o);
+        default: return triangle_hit(c.p, O, D, o);
+    }
+}
+
+// ---- normals and uv (per collider) ---------------------------------------------------------
+// cuboid.py:142-151: face normal picked by the largest scaled |local coordinate|
+RT_HD d3 cuboid_normal(const double* p, d3 P) {
+    d3 L = matmul_rows(p + 3, sub(P, ld3(p)));
+    double ax = p[39] * fabs(L.x), ay = p[40] * fabs(L.y), az = p[41] * fabs(L.z);
+    double m = np_max(np_max(ax, ay), az);
+    d3 s = d3{m == ax ? np_sign(L.x) : 0.0, m == ay ? np_sign(L.y) : 0.0, m == az ? np_sign(L.z) : 0.0};
+    return matmul_rows(p + 30, s);
+}
+
+// un-oriented collider normal at P (Collider.get_Normal)
+RT_HD d3 collider_normal(const srt_collider& c, d3 P) {
+    switch (c.type) {
+        case SRT_SPHERE: return mul(sub(P, ld3(c.p)), c.p[4]);  // sphere.py:54-56
+        case SRT_PLANE: return ld3(c.p + 3);                       // plane.py:104-105
+        case SRT_CUBOID: return cuboid_normal(c.p, P);
+        default: return ld3(c.p + 3);                              // triangle.py:85-86
+    }
+}
+
+// cuboid.py:153-187: 4x3 cube-cross coordinates; every face divides by `width`
+RT_HD double cross_coord(d3 ax, double sgn, d3 MC, double width, double shift) {
+    d3 a = d3{ax.x * sgn, ax.y * sgn, ax.z * sgn};
+    return ((((dot(a, MC) / width) * 2.0) * 0.985 + 1.0) / 2.0) + shift;
+}
+RT_HD void cuboid_uv(const double* p, d3 P, double& u, double& v) {
+    d3 N = cuboid_normal(p, P);
+    d3 MC = sub(P, ld3(p));
+    d3 aw = ld3(p + 18), ah = ld3(p + 21), al = ld3(p + 24);
+    double w = p[27];
+    if (N.x == 0.0 && N.y == -1.0 && N.z == 0.0) {  // BOTTOM
+        u = cross_coord(aw, 1.0, MC, w, 1.0); v = cross_coord(al, -1.0, MC, w, 0.0);
+    } else if (N.x == 0.0 && N.y == 1.0 && N.z == 0.0) {  // TOP
+        u = cross_coord(aw, 1.0, MC, w, 1.0); v = cross_coord(al, 1.0, MC, w, 2.0);
+    } else if (N.x == 1.0 && N.y == 0.0 && N.z == 0.0) {  // RIGHT
+        u = cross_coord(al, 1.0, MC, w, 2.0); v = cross_coord(ah, 1.0, MC, w, 1.0);
+    } else if (N.x == -1.0 && N.y == 0.0 && N.z == 0.0) {  // LEFT
+        u = cross_coord(al, -1.0, MC, w, 0.0); v = cross_coord(ah, 1.0, MC, w, 1.0);
+    } else if (N.x == 0.0 && N.y == 0.0 && N.z == 1.0) {  // FRONT
+        u = cross_coord(aw, -1.0, MC, w, 3.0); v = cross_coord(ah, 1.0, MC, w, 1.0);
+    } else if (N.x == 0.0 && N.y == 0.0 && N.z == -1.0) {  // BACK
+        u = cross_coord(aw, 1.0, MC, w, 1.0); v = cross_coord(ah, 1.0, MC, w, 1.0);
+    } else {  // np.select default
+        u = 0.0; v = 0.0;
+    }
+}
+
+// Primitive.get_uv(hit) for the collider's primitive; returns false for the undefined Triangle uv
+RT_HD bool collider_uv(const srt_collider& c, d3 P, double& u, double& v) {
+    switch (c.type) {
+        case SRT_SPHERE: {  // sphere.py:58-64
+            d3 M = divs(sub(P, ld3(c.p)), c.p[3]);
+            u = (atan2(M.z, M.x) + PI) / TWO_PI;
+            v = (asin(M.y) + HALF_PI) / PI;
+            break;
+        }
+        case SRT_PLANE: {  // plane.py:98-102
+            d3 MC = sub(P, ld3(c.p));
+            u = (dot(ld3(c.p + 6), MC) / c.p[12] + 1.0) / 2.0 + c.p[14];
+            v = (dot(ld3(c.p + 9), MC) / c.p[13] + 1.0) / 2.0 + c.p[15];
+            break;
+        }
+        case SRT_CUBOID: cuboid_uv(c.p, P, u, v); break;
+        default: u = 0.0; v = 0.0; return false;
+    }
+    if (c.flags & SRT_CF_UV_CROSS) {  // cuboid.py:29-32, skybox.py:29-32
+        u = u / 4.0;
+        v = v / 3.0;
+    }
+    return true;
+}
+
+// ---- textures -------------------------------------------------------------------------------
+// numpy fancy-index semantics for one axis: -n <= i < n, negative wraps
+RT_HD int64_t np_index(int64_t i, int64_t n, uint32_t& err) {
+    if (i < 0) i += n;
+    if (i < 0 || i >= n) {
+        err |= ERR_INDEX;
+        i = i < 0 ? 0 : n - 1;
+    }
+    return i;
+}
+RT_HD const uint8_t* texel_at(const SceneView& S, const srt_texture& T, int64_t row, int64_t col, uint32_t& err) {
+    row = np_index(row, T.height, err);
+    col = np_index(col, T.width, err);
+    return S.texels + T.offset + (row * (int64_t)T.width + col) * T.channels + T.channel0;
+}
+// img[-(int(v*H*rep) % H), int(u*W*rep) % W] (texture.py:32-39, skybox.py:54-86)
+RT_HD const uint8_t* tex_uv(const SceneView& S, const srt_texture& T, double u, double v, uint32_t& err) {
+    int64_t m = py_mod(np_trunc((v * (double)T.idx_h) * T.repeat), T.idx_h);
+    int64_t col = py_mod(np_trunc((u * (double)T.idx_w) * T.repeat), T.idx_w);
+    return texel_at(S, T, -m, col, err);
+}
+RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err) {
+    const srt_texture& T = S.tex[tid];
+    const uint8_t* px = tex_uv(S, T, u, v, err);
+    return d3{T.lut[px[0]], T.lut[px[1]], T.lut[px[2]]};
+}
+
+// Material.get_Normal (material.py:18-36): collider normal (or normal map) times orientation
+RT_HD d3 shading_normal(const SceneView& S, const srt_collider& c, const srt_material& m, d3 P,
+                        double orient, uint32_t& err) {
+    if (m.normalmap >= 0) {
+        double u, v;
+        if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+        const srt_texture& T = S.tex[m.normalmap];
+        const uint8_t* px = tex_uv(S, T, u, v, err);
+        d3 nm = d3{(T.lut[px[0]] - 0.5) * 2.0, (T.lut[px[1]] - 0.5) * 2.0, (T.lut[px[2]] - 0.5) * 2.0};
+        const double* ib = (c.type == SRT_PLANE) ? c.p + 16 : c.p + 30;
+        return mul(normalize(matmul_rows(ib, nm)), orient);
+    }
+    return mul(collider_normal(c, P), orient);
+}
+
+// ---- counter-based RNG (Philox4x32-10) for Monte-Carlo shading and device jitter -------------
+struct u4 {
+    uint32_t a, b, c, d;
+};
+RT_HD uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+RT_HD u4 philox(u4 ctr, uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        uint32_t h0 = mulhi32(0xD2511F53u, ctr.a), l0 = 0xD2511F53u * ctr.a;
+        uint32_t h1 = mulhi32(0xCD9E8D57u, ctr.c), l1 = 0xCD9E8D57u * ctr.c;
+        ctr = u4{h1 ^ ctr.b ^ k0, l1, h0 ^ ctr.d ^ k1, l0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return ctr;
+}
+// numpy's 53-bit double from two 32-bit words
+RT_HD double u01(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
+struct Rng {
+    uint32_t k0, k1, c0, c1, c2, n;
+    RT_HDM void init(uint64_t seed, uint32_t pix, uint32_t path, uint32_t tag) {
+        k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); c0 = pix; c1 = path; c2 = tag; n = 0;
+    }
+    RT_HDM void two(double& x, double& y) {
+        u4 r = philox(u4{c0, c1, c2, n++}, k0, k1);
+        x = u01(r.a, r.b);
+        y = u01(r.c, r.d);
+    }
+    RT_HDM double one() {
+        double x, y;
+        two(x, y);
+        return x;
+    }
+};
+RT_HD uint32_t mix32(uint32_t h, uint32_t v) {
+    h ^= v + 0x9E3779B9u + (h << 6) + (h >> 2);
+    h *= 0x85EBCA6Bu;
+    return h ^ (h >> 13);
+}
+
+// ---- rays -----------------------------------------------------------------------------------
+// meta word: medium (8) | depth (8) | diffuse reflections (8)
+RT_HD uint32_t pack_meta(uint32_t medium, uint32_t depth, uint32_t diffuse) {
+    return (medium & 0xFFu) | ((depth & 0xFFu) << 8) | ((diffuse & 0xFFu) << 16);
+}
+RT_HD uint32_t meta_medium(uint32_t m) { return m & 0xFFu; }
+RT_HD uint32_t meta_depth(uint32_t m) { return (m >> 8) & 0xFFu; }
+RT_HD uint32_t meta_diffuse(uint32_t m) { return (m >> 16) & 0xFFu; }
+
+struct Ray {
+    d3 o, d, w;  // origin, direction, throughput (product of the Fresnel/absorption weights)
+    uint32_t pix, meta, path;
+};
+
+// Camera.get_ray for one pixel (camera.py:51-85, utils/random.py:6-9)
+RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double j[4], d3& O, d3& D) {
+    double x = xc + ((j[0] - 0.5) * cam.cam_width) / (double)cam.width;
+    double y = yr + ((j[1] - 0.5) * cam.cam_height) / (double)cam.height;
+    double r = sqrt(j[2]);
+    double phi = (j[3] * 2.0) * PI;
+    double rx = r * cos(phi), ry = r * sin(phi);
+    d3 lf = ld3(cam.look_from), R = ld3(cam.right), U = ld3(cam.up);
+    O = add(add(lf, mul(mul(R, rx), cam.lens_radius)), mul(mul(U, ry), cam.lens_radius));
+    d3 t = add(add(add(lf, mul(mul(U, y), cam.focal_distance)), mul(mul(R, x), cam.focal_distance)),
+               ld3(cam.fwd_fd));
+    D = normalize(sub(t, O));
+}
+
+// Nearest collider over the scene (ray.py:124-132): nearest = reduce(np.minimum, distances);
+// a collider is hit where nearest != FARAWAY and its distance == nearest.  Returns the first
+// such collider (-1 if none); `ties` reports that a later collider hit at the same distance.
+RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bool& ties) {
+    double best = FARAWAY;
+    int id = -1;
+    double bo = FARAWAY;
+    ties = false;
+    bool nan = false;
+    for (int c = 0; c < S.ncol; ++c) {
+        double o;
+        double t = collider_hit(S.col[c], O, D, o);
+        if (t != t) nan = true;
+        if (t < best) { best = t; id = c; bo = o; ties = false; }
+        else if (t == best && id >= 0) ties = true;
+    }
+    if (nan || best == FARAWAY) { tn = nan ? NAN : FARAWAY; on = FARAWAY; ties = false; return -1; }
+    tn = best;
+    on = bo;
+    return id;
+}
+
+// ---- shading --------------------------------------------------------------------------------
+// Shading functions report their results to an emitter `E` as they are produced:
+//   em.local(c)        colour added at this hit (the caller multiplies by the ray throughput)
+//   em.child(ch)       one child ray (weight relative to the parent's throughput)
+//   em.diffuse(g, m)   a Diffuse fan-out of g.count children (generated by diffuse_child)
+//   em.shadow(n)       n shadow rays were traced
+// On the GPU the emitter appends children with one atomic per wave (rt_kernels.hip); in the host
+// check harness it pushes to a vector.  Nothing is held per lane between hits.
+struct Child {
+    d3 o, d, w;       // w: weight relative to the parent's throughput
+    uint32_t medium;  // media row the child travels in
+    uint32_t dfl;     // diffuse reflections of the child
+    uint32_t slot;    // child index (path hash)
+};
+// Diffuse fan-out descriptor
+struct DiffuseGen {
+    d3 P;       // nudged origin
+    d3 N;       // oriented normal
+    d3 w;       // diff colour / (pi * count)
+    int count;  // diffuse_rays (first bounce) or 1
+    uint32_t medium, dfl;
+};
+
+RT_HD d3 schlick(d3 F0, double cos_t) {
+    double p = pow(1.0 - cos_t, 5.0);
+    d3 one_m = rsub(1.0, F0);
+    return add(F0, mul(one_m, p));
+}
+
+RT_HD d3 reflect_dir(d3 D, d3 N) {
+    double dn = dot(D, N);
+    d3 N2 = mul(N, 2.0);
+    return normalize(sub(D, mul(N2, dn)));
+}
+
+RT_HD Child mkchild(d3 o, d3 d, d3 w, uint32_t medium, uint32_t dfl, uint32_t slot) {
+    Child c;
+    c.o = o; c.d = d; c.w = w; c.medium = medium; c.dfl = dfl; c.slot = slot;
+    return c;
+}
+
+// min over the shadowed colliders of the distance along the light direction (glossy.py:53-59)
+RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L) {
+    double best = FARAWAY;
+    bool first = true;
+    for (int c = 0; c < S.ncol; ++c) {
+        const srt_collider& cc = S.col[c];
+        if (!(cc.flags & SRT_CF_SHADOW)) continue;
+        double o, t;
+        if (cc.type == SRT_CUBOID)
+            t = cuboid_hit_local(cc.p, O, ld3(S.light_local + ((int64_t)light * S.ncol + c) * 3), o);
+        else
+            t = collider_hit(cc, O, L, o);
+        best = first ? t : np_min(best, t);
+        first = false;
+    }
+    return best;
+}
+
+// Glossy.get_color (glossy.py:25-110)
+template <class E>
+RT_HD void shade_glossy(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, double orient,
+                        E& em, uint32_t& err) {
+    const srt_material& m = S.mat[mi];
+    d3 P = add(r.o, mul(r.d, t));
+    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 diff;
+    if (m.tex >= 0) {
+        double u, v;
+        if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+        diff = mul(tex_rgb(S, m.tex, u, v, err), m.p[3]);
+    } else {
+        diff = ld3(m.p);
+    }
+    d3 color = mul(ld3(S.ambient), diff);
+    d3 V = mul(r.d, -1.0);
+    d3 nudged = add(P, mul(N, NUDGE));
+    uint32_t med = meta_medium(r.meta);
+    for (int l = 0; l < S.nlights; ++l) {
+        const srt_light& Lt = S.lights[l];
+        d3 L, lv;
+        double dist;
+        if (Lt.type == SRT_LIGHT_DIRECTIONAL) {
+            L = ld3(Lt.dir);
+            dist = SKYBOX_DISTANCE;
+        } else {  // point light, evident intent of lights.py:23-37 (parity unpinned)
+            d3 toL = sub(ld3(Lt.pos), P);
+            dist = sqrt(dot(toL, toL));
+            L = mul(toL, 1.0 / dist);
+        }
+        double NdotL = np_max(dot(N, L), 0.0);
+        lv = mul(ld3(Lt.color), NdotL);
+        if (Lt.type != SRT_LIGHT_DIRECTIONAL) lv = mul(divs(lv, dist * dist), 100.0);
+        d3 H = normalize(add(L, V));
+        double seelight = 1.0;
+        if (S.nshadow > 0) {
+            double ln = shadow_nearest(S, l, nudged, L);
+            seelight = (ln >= dist) ? 1.0 : 0.0;
+            em.shadow(1);
+        }
+        color = add(color, mul(mul(diff, lv), seelight));
+        if (m.flags & SRT_MF_ROUGH) {
+            d3 F0 = ld3(S.glossy_f0 + ((int64_t)mi * S.nmedia + med) * 3);
+            double cos_t = np_clip(dot(V, H), 0.0, 1.0);
+            d3 F = schlick(F0, cos_t);
+            double Dphong = (pow(np_clip(dot(N, H), 0.0, 1.0), m.p[4]) * m.p[5]) / m.p[6];
+            double den = 4.0 * np_clip(dot(N, V) * NdotL, 0.001, 1.0);
+            d3 spec = mul(mul(mul(divs(mul(F, Dphong), den), seelight), lv), m.p[7]);
+            color = add(color, spec);
+        }
+    }
+    em.local(color);
+    if ((int)meta_depth(r.meta) < c.max_ray_depth) {
+        double cos_t = np_clip(dot(V, N), 0.0, 1.0);
+        d3 F = schlick(ld3(m.p + 8), cos_t);
+        em.child(mkchild(nudged, reflect_dir(r.d, N), F, med, meta_diffuse(r.meta), 1));
+    }
+}
+
+// Refractive.get_color (refractive.py:24-123); `mc_u` is the uniform for the MC pick
+template <class E>
+RT_HD void shade_refractive(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t,
+                            double orient, E& em, uint32_t& err, double mc_u) {
+    if ((int)meta_depth(r.meta) >= c.max_ray_depth) return;  // black beyond max_ray_depth
+    const srt_material& m = S.mat[mi];
+    d3 P = add(r.o, mul(r.d, t));
+    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 V = mul(r.d, -1.0);
+    uint32_t m1 = meta_medium(r.meta);
+    uint32_t m2 = (orient == 1.0) ? (uint32_t)m.medium : 0u;
+    const double* n1 = S.media + m1 * 6;
+    const double* n2 = S.media + m2 * 6;
+    double cos_i = dot(V, N);
+    double s = 1.0 - cos_i * cos_i;
+    double F[3], ratio[3];
+    for (int k = 0; k < 3; ++k) {
+        cplx a1 = cplx{n1[k], n1[3 + k]}, a2 = cplx{n2[k], n2[3 + k]};
+        ratio[k] = n1[k] / n2[k];
+        cplx q = cdiv(a1, a2);
+        cplx z = cmulr(cmul(q, q), s);
+        cplx cos_t = csqrt_np(cplx{1.0 - z.re, 0.0 - z.im});
+        cplx x1 = cmulr(a1, cos_i), x2 = cmul(a2, cos_t);
+        cplx r_per = cdiv(csub(x1, x2), cadd(x1, x2));
+        cplx y1 = cmul(a1, cos_t), y2 = cmulr(a2, cos_i);
+        cplx r_par = cdiv(cmul(cplx{-1.0, 0.0}, csub(y1, y2)), cadd(y1, y2));
+        double ap = cabs(r_per), aq = cabs(r_par);
+        F[k] = (ap * ap + aq * aq) / 2.0;
+    }
+    // absorption: exp(-2 * Im(n_ray) * 2 * pi / lambda * 1e9 * distance), lambda = (630, 550, 475)
+    const double lam[3] = {630.0, 550.0, 475.0};
+    double ab[3];
+    for (int k = 0; k < 3; ++k) ab[k] = exp(((((-2.0 * n1[3 + k]) * 2.0) * PI) / lam[k]) * 1e9 * t);
+    double aver = ((ratio[0] + ratio[1]) + ratio[2]) / 3.0;
+    double sin2 = (aver * aver) * (1.0 - cos_i * cos_i);
+    bool non_tir = sin2 <= 1.0;
+    uint32_t dfl = meta_diffuse(r.meta);
+    if (c.flags & SRT_CF_MC) {
+        double favg = ((F[0] + F[1]) + F[2]) / 3.0;
+        bool refr = (mc_u > favg) && non_tir;
+        d3 w = d3{ab[0], ab[1], ab[2]};
+        if (refr) {
+            double kk = aver * cos_i - sqrt(1.0 - np_clip(sin2, 0.0, 1.0));
+            d3 Rt = normalize(add(mul(r.d, aver), mul(N, kk)));
+            em.child(mkchild(sub(P, mul(N, NUDGE)), Rt, w, m2, dfl, 1));
+        } else {
+            em.child(mkchild(add(P, mul(N, NUDGE)), reflect_dir(r.d, N), w, m1, dfl, 1));
+        }
+        return;
+    }
+    em.child(mkchild(add(P, mul(N, NUDGE)), reflect_dir(r.d, N), d3{F[0] * ab[0], F[1] * ab[1], F[2] * ab[2]},
+                     m1, dfl, 1));
+    if (non_tir) {
+        double kk = aver * cos_i - sqrt(1.0 - np_clip(sin2, 0.0, 1.0));
+        d3 Rt = normalize(add(mul(r.d, aver), mul(N, kk)));
+        em.child(mkchild(sub(P, mul(N, NUDGE)), Rt,
+                         d3{(1.0 - F[0]) * ab[0], (1.0 - F[1]) * ab[1], (1.0 - F[2]) * ab[2]}, m2, dfl, 2));
+    }
+}
+
+// ThinFilmInterference.get_color (thin_film_interference.py:24-115)
+template <class E>
+RT_HD void shade_thinfilm(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t,
+                          double orient, E& em, uint32_t& err) {
+    if ((int)meta_depth(r.meta) >= c.max_ray_depth) return;
+    const srt_material& m = S.mat[mi];
+    d3 P = add(r.o, mul(r.d, t));
+    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 V = mul(r.d, -1.0);
+    double cos_i = dot(V, N);
+    const srt_texture& lut = S.tex[m.tex_aux0];
+    int64_t li = np_trunc(cos_i * (double)lut.height);
+    int64_t ti;
+    if (m.flags & SRT_MF_NOISE) {
+        double u, v;
+        if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+        const srt_texture& nt = S.tex[m.tex_aux1];
+        double nz = nt.lut[*tex_uv(S, nt, u, v, err)];
+        double thick = m.p[0] + m.p[1] * (nz - 0.5);
+        ti = np_trunc(thick);
+    } else {
+        ti = (int64_t)m.p[0];
+    }
+    const uint8_t* px = texel_at(S, lut, li, ti, err);
+    d3 F = d3{lut.lut[px[0]], lut.lut[px[1]], lut.lut[px[2]]};
+    em.local(mul(ld3(S.ambient), F));
+    uint32_t med = meta_medium(r.meta), dfl = meta_diffuse(r.meta);
+    em.child(mkchild(add(P, mul(N, NUDGE)), reflect_dir(r.d, N), F, med, dfl, 1));
+    em.child(mkchild(sub(P, mul(N, NUDGE)), r.d, rsub(1.0, F), med, dfl, 2));
+}
+
+// SkyBox_Material.get_texture_color (skybox.py:51-94)
+template <class E>
+RT_HD void shade_sky(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, E& em,
+                     uint32_t& err) {
+    const srt_material& m = S.mat[mi];
+    d3 P = add(r.o, mul(r.d, t));
+    double u, v;
+    if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+    d3 col = tex_rgb(S, m.tex, u, v, err);
+    if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP)) {
+        const srt_texture& L = S.tex[m.tex_aux0];
+        const uint8_t* px = tex_uv(S, L, u, v, err);
+        col = d3{col.x + m.p[0] * L.lut[px[0]], col.y + m.p[0] * L.lut[px[1]], col.z + m.p[0] * L.lut[px[2]]};
+    }
+    em.local(col);
+}
+
+// Emissive.get_color (emissive.py:21-23)
+template <class E>
+RT_HD void shade_emissive(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, E& em,
+                          uint32_t& err) {
+    const srt_material& m = S.mat[mi];
+    if (m.tex >= 0) {
+        double u, v;
+        d3 P = add(r.o, mul(r.d, t));
+        if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+        em.local(tex_rgb(S, m.tex, u, v, err));
+    } else {
+        em.local(ld3(m.p));
+    }
+}
+
+// Diffuse.get_color (diffuse.py:25-124): no local colour; the children carry the estimate
+template <class E>
+RT_HD void shade_diffuse(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, double orient,
+                         E& em, uint32_t& err) {
+    uint32_t dfl = meta_diffuse(r.meta);
+    if (dfl >= 2) return;
+    const srt_material& m = S.mat[mi];
+    d3 P = add(r.o, mul(r.d, t));
+    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 diff;
+    if (m.tex >= 0) {
+        double u, v;
+        if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+        diff = tex_rgb(S, m.tex, u, v, err);
+    } else {
+        diff = ld3(m.p);
+    }
+    DiffuseGen g;
+    g.count = (dfl < 1) ? m.ival : 1;
+    g.P = add(P, mul(N, NUDGE));
+    g.N = N;
+    g.w = mul(diff, 1.0 / (PI * (double)g.count));
+    g.medium = meta_medium(r.meta);
+    g.dfl = dfl + 1;
+    em.diffuse(g, mi);
+}
+
+// ONB of utils/random.py:72-76 (ax_w given)
+RT_HD void onb(d3 w, d3& u, d3& v) {
+    d3 a = (fabs(w.x) > 0.9) ? d3{0.0, 1.0, 0.0} : d3{1.0, 0.0, 0.0};
+    d3 c = d3{w.y * a.z - w.z * a.y, -w.x * a.z + w.z * a.x, w.x * a.y - w.y * a.x};
+    v = normalize(c);
+    u = d3{w.y * v.z - w.z * v.y, -w.x * v.z + w.z * v.x, w.x * v.y - w.y * v.x};
+}
+
+// One diffuse child: direction from the cosine PDF or the cosine/spherical-caps mixture
+// (utils/random.py:58-174), weight = w * clip(N.d) / pdf(d).
+RT_HD Child diffuse_child(const SceneView& S, const srt_material& m, const DiffuseGen& g, Rng& rng, uint32_t k) {
+    double pdf1w = m.p[3];
+    double sel, dummy;
+    rng.two(sel, dummy);
+    bool caps = (S.nimp > 0) && !(sel < pdf1w);
+    d3 dir;
+    if (!caps) {
+        d3 u, v;
+        onb(g.N, u, v);
+        double a, b;
+        rng.two(a, b);
+        double phi = (a * 2.0) * PI;
+        double z = sqrt(1.0 - b), x = cos(phi) * sqrt(b), y = sin(phi) * sqrt(b);
+        dir = add(add(mul(u, x), mul(v, y)), mul(g.N, z));
+    } else {
+        double pick, a;
+        rng.two(pick, a);
+        int i = (int)(pick * (double)S.nimp);
+        if (i >= S.nimp) i = S.nimp - 1;
+        const double* im = S.importance + 4 * i;
+        d3 tc = sub(ld3(im), g.P);
+        d3 w = normalize(tc);
+        double dist = sqrt(dot(tc, tc));
+        double rr = np_clip(im[3] / dist, 0.0, 1.0);
+        double cmax = sqrt(1.0 - rr * rr);
+        d3 u, v;
+        onb(w, u, v);
+        double b = rng.one();
+        double phi = (a * 2.0) * PI;
+        double z = 1.0 + b * (cmax - 1.0);
+        double sz = sqrt(1.0 - z * z);
+        dir = add(add(mul(u, cos(phi) * sz), mul(v, sin(phi) * sz)), mul(w, z));
+    }
+    double cosp = np_clip(dot(dir, g.N), 0.0, 1.0) / PI;
+    double pdf = cosp;
+    if (S.nimp > 0) {
+        double caps_pdf = 0.0;
+        for (int i = 0; i < S.nimp; ++i) {
+            const double* im = S.importance + 4 * i;
+            d3 tc = sub(ld3(im), g.P);
+            d3 w = normalize(tc);
+            double dist = sqrt(dot(tc, tc));
+            double rr = np_clip(im[3] / dist, 0.0, 1.0);
+            double cmax = sqrt(1.0 - rr * rr);
+            if (dot(dir, w) > cmax) caps_pdf += 1.0 / ((1.0 - cmax) * TWO_PI);
+        }
+        caps_pdf = caps_pdf / (double)S.nimp;
+        pdf = cosp * pdf1w + caps_pdf * m.p[4];
+    }
+    double ndl = np_clip(dot(dir, g.N), 0.0, 1.0);
+    return mkchild(g.P, dir, mul(g.w, ndl / pdf), g.medium, g.dfl, 0x100u + k);
+}
+
+// Shade one (ray, collider) hit with a per-lane (possibly divergent) material.
+template <class E>
+RT_HD void shade_hit(const SceneView& S, int cid, int mi, const Ray& r, double t, double orient, E& em,
+                     uint32_t& err, double mc_u) {
+    const srt_collider& c = S.col[cid];
+    switch (S.mat[mi].type) {
+        case SRT_GLOSSY: shade_glossy(S, c, mi, r, t, orient, em, err); break;
+        case SRT_REFRACTIVE: shade_refractive(S, c, mi, r, t, orient, em, err, mc_u); break;
+        case SRT_THINFILM: shade_thinfilm(S, c, mi, r, t, orient, em, err); break;
+        case SRT_DIFFUSE: shade_diffuse(S, c, mi, r, t, orient, em, err); break;
+        case SRT_EMISSIVE: shade_emissive(S, c, mi, r, t, em, err); break;
+        default: shade_sky(S, c, mi, r, t, em, err); break;
+    }
+}
+
+// RNG stream of the Monte-Carlo refraction pick / diffuse children of a ray
+RT_HD uint32_t child_path(uint32_t path, uint32_t slot, uint32_t round) { return mix32(path, slot + 4096u * round); }
+
+// sRGB_linear_to_sRGB + clip + uint8 for one pixel (colour_functions.py:4-18, scene.py:125-140)
+RT_HD void resolve_pixel(double r, double g, double b, double& orr, double& og, double& ob, uint8_t px[3]) {
+    double c[3] = {r, g, b}, e[3];
+    for (int k = 0; k < 3; ++k)
+        e[k] = (c[k] <= 0.00304) ? 12.92 * c[k] : 1.055 * pow(c[k], 1.0 / 2.4) - 0.055;
+    double peak = np_max(np_max(e[0], e[1]), e[2]) + 0.00001;
+    if (peak > 1.0)
+        for (int k = 0; k < 3; ++k) e[k] = (e[k] * 1.0) / peak;
+    for (int k = 0; k < 3; ++k) {
+        double q = 255.0 * np_clip(e[k], 0.0, 1.0);
+        px[k] = (q == q) ? (uint8_t)(int)q : (uint8_t)0;
+    }
+    orr = r; og = g; ob = b;
+}
+
+}  // namespace rt

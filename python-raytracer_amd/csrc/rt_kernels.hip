@@ -1,0 +1,940 @@
+// rt_kernels.hip -- gfx950 wavefront tracer behind the C ABI of include/sightpy_rt.h.
+//
+// The reference (sightpy) recursively evaluates numpy batches: intersect every collider, reduce
+// the nearest hit, compact the rays per collider, shade, recurse (ray.py:122-148).  Here the
+// recursion is flattened into a breadth-first wavefront over structure-of-arrays ray queues in
+// HBM, one launch per depth:
+//
+//   k_trace<true>  depth 0: primary-ray generation (camera.py:51-85) fused with the trace step
+//   k_trace<false> depth d: read ray d from queue, nearest hit over all colliders, shade,
+//                  add throughput * local colour to the framebuffer, append children to d+1
+//   k_resolve      spp average + sRGB + intensity clip + uint8 (scene.py:118-140)
+//
+// A colour composes linearly along the ray tree (colour = local + F * child), so each queued ray
+// carries the product of the weights above it (its throughput) and contributions are summed into
+// the per-pixel framebuffer with float64 atomics.  Scene tables are read through wave-uniform
+// indices (scalar loads) in the collider loop; shading runs as a waterfall over the materials
+// present in a wave so each material's parameters are wave-uniform too.  Children are appended
+// with one block-wide exclusive scan and one atomicAdd per block.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_device.h"
+
+using namespace rt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return fail(SRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));        \
+    } while (0)
+
+constexpr int BLOCK = 256;
+constexpr int NSHARD = 16;  // queue shards: one append counter per shard (blocks b, b+16, ... share one)
+
+struct Queue {
+    double *ox, *oy, *oz, *dx, *dy, *dz, *wr, *wg, *wb;
+    uint32_t *pix, *meta, *path;
+};
+constexpr int64_t RAY_BYTES = 9 * 8 + 3 * 4;  // 84 B per queued ray
+
+struct TraceParams {
+    SceneView S;
+    Queue qin, qout;
+    const uint32_t* cnt_in;  // [NSHARD] rays per input shard (depth d)
+    uint32_t* cnt_out;       // [NSHARD] append counters of the output shards (depth d+1)
+    uint32_t* flags;         // [0] error bits, [1] overflow
+    unsigned long long* shadow;
+    double* fb;              // [3][npix]
+    int64_t npix;
+    int64_t seg;             // capacity of one queue shard (rays)
+    uint64_t seed;
+    int depth;
+    // primary generation
+    int64_t n_primary;
+    srt_camera cam;
+    const int32_t* rows;
+    const double* jitter;  // [spp][4][npix] (device) or null
+    int sample_base;
+    int32_t* hit_out;  // [spp][npix] or null
+};
+
+__device__ __forceinline__ void queue_store(const Queue& q, int64_t i, d3 o, d3 d, d3 w, uint32_t pix,
+                                            uint32_t meta, uint32_t path) {
+    q.ox[i] = o.x; q.oy[i] = o.y; q.oz[i] = o.z;
+    q.dx[i] = d.x; q.dy[i] = d.y; q.dz[i] = d.z;
+    q.wr[i] = w.x; q.wg[i] = w.y; q.wb[i] = w.z;
+    q.pix[i] = pix; q.meta[i] = meta; q.path[i] = path;
+}
+
+__device__ __forceinline__ Ray queue_load(const Queue& q, int64_t i) {
+    Ray r;
+    r.o = d3{q.ox[i], q.oy[i], q.oz[i]};
+    r.d = d3{q.dx[i], q.dy[i], q.dz[i]};
+    r.w = d3{q.wr[i], q.wg[i], q.wb[i]};
+    r.pix = q.pix[i]; r.meta = q.meta[i]; r.path = q.path[i];
+    return r;
+}
+
+__device__ __forceinline__ void fb_add(double* fb, int64_t npix, uint32_t pix, d3 w, d3 c) {
+    if (is_zero(c)) return;  // adding an exact zero is a no-op (framebuffer starts at +0.0)
+    unsafeAtomicAdd(fb + pix, w.x * c.x);
+    unsafeAtomicAdd(fb + npix + pix, w.y * c.y);
+    unsafeAtomicAdd(fb + 2 * npix + pix, w.z * c.z);
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Reserve `cnt` consecutive slots of the output shard for every active lane: one atomic per wave.
+// The exclusive prefix of the (small) per-lane counts is assembled from one ballot per bit, which
+// is exact in divergent code (inactive lanes contribute nothing).
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t cnt) {
+    uint32_t total = 0, below = 0;
+    uint64_t any = __ballot(cnt != 0);
+    if (!any) return 0;
+    for (int b = 0; b < 8; ++b) {
+        uint64_t m = __ballot((cnt >> b) & 1u);
+        total += (uint32_t)__builtin_popcountll(m) << b;
+        below += lanes_below(m) << b;
+    }
+    uint32_t base = 0;
+    if (lanes_below(__ballot(1)) == 0) base = atomicAdd(ctr, total);  // first active lane
+    base = __builtin_amdgcn_readfirstlane(base);
+    return base + below;
+}
+
+// Emitter of the GPU trace step: colour -> framebuffer atomics, children -> output queue shard.
+struct GpuEmit {
+    const TraceParams& P;
+    const Ray& r;
+    uint32_t shard;
+    uint32_t round;
+    uint32_t* shadow_acc;
+
+    __device__ void local(d3 c) const { fb_add(P.fb, P.npix, r.pix, r.w, c); }
+    __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
+    __device__ void store(uint32_t slot, const Child& c, uint32_t path) const {
+        if (slot < (uint64_t)P.seg) {
+            queue_store(P.qout, (int64_t)shard * P.seg + slot, c.o, c.d, mul(r.w, c.w), r.pix,
+                        pack_meta(c.medium, meta_depth(r.meta) + 1, c.dfl), path);
+        } else {
+            P.flags[1] = 1u;
+        }
+    }
+    __device__ void child(const Child& c) const {
+        uint32_t slot = wave_reserve(P.cnt_out + shard, 1u);
+        store(slot, c, child_path(r.path, c.slot, round));
+    }
+    __device__ void diffuse(const DiffuseGen& g, int mi) const {
+        uint32_t slot = wave_reserve(P.cnt_out + shard, (uint32_t)g.count);
+        const srt_material& m = P.S.mat[mi];
+        for (int k = 0; k < g.count; ++k) {
+            Rng rng;
+            const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
+            rng.init(P.seed, r.pix, cpath, 0xD1000000u | (uint32_t)P.depth);
+            store(slot + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
+        }
+    }
+};
+
+__device__ __forceinline__ double mc_uniform(const TraceParams& P, const Ray& r, int cid, uint32_t round) {
+    if (!(P.S.col[cid].flags & SRT_CF_MC)) return 0.0;
+    Rng g;
+    g.init(P.seed, r.pix, r.path, 0x3C000000u | ((uint32_t)P.depth << 8) | round);
+    return g.one();
+}
+
+// Uniforms for primary ray of sample s at local pixel p.
+__device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, uint32_t p, uint32_t gpix,
+                                                 double j[4]) {
+    if (P.jitter) {
+        const double* base = P.jitter + (int64_t)s * 4 * P.npix + p;
+        j[0] = base[0]; j[1] = base[P.npix]; j[2] = base[2 * P.npix]; j[3] = base[3 * P.npix];
+    } else {
+        Rng g;
+        g.init(P.seed, gpix, (uint32_t)(P.sample_base + s), 0xCA3E0000u);
+        g.two(j[0], j[1]);
+        g.two(j[2], j[3]);
+    }
+}
+
+// One trace step for one ray (all lanes of the wave call it; `active` masks the tail).
+__device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool active, uint32_t shard, uint32_t& err,
+                                          uint32_t& shadow, int32_t* hit_slot) {
+    const SceneView& S = P.S;
+    double t = FARAWAY, o = FARAWAY;
+    bool ties = false;
+    int id = -1;
+    if (active) id = nearest_hit(S, r.o, r.d, t, o, ties);
+    if (hit_slot && active) *hit_slot = id;
+    const int mat = (id >= 0) ? S.col[id].material : -1;
+    GpuEmit em{P, r, shard, 0u, &shadow};
+    // waterfall over the materials present in the wave: material index and its parameters are
+    // wave-uniform inside each pass (scalar loads, uniform type switch)
+    uint64_t pending = __ballot(mat >= 0);
+    while (pending) {
+        const int lead = __builtin_ctzll(pending);
+        const int m = __builtin_amdgcn_readfirstlane(__shfl(mat, lead));
+        const bool mine = (mat == m);
+        if (mine) {
+            const srt_collider& c = S.col[id];
+            switch (S.mat[m].type) {
+                case SRT_GLOSSY: shade_glossy(S, c, m, r, t, o, em, err); break;
+                case SRT_REFRACTIVE: shade_refractive(S, c, m, r, t, o, em, err, mc_uniform(P, r, id, 0)); break;
+                case SRT_THINFILM: shade_thinfilm(S, c, m, r, t, o, em, err); break;
+                case SRT_DIFFUSE: shade_diffuse(S, c, m, r, t, o, em, err); break;
+                case SRT_EMISSIVE: shade_emissive(S, c, m, r, t, em, err); break;
+                default: shade_sky(S, c, m, r, t, em, err); break;
+            }
+        }
+        pending &= ~__ballot(mine);
+    }
+    // colliders tied at the same distance are all shaded and their colours added (ray.py:131-146)
+    if (ties) {
+        uint32_t round = 1;
+        for (int c = id + 1; c < S.ncol; ++c) {
+            double oc;
+            if (collider_hit(S.col[c], r.o, r.d, oc) == t) {
+                GpuEmit et{P, r, shard, round++, &shadow};
+                shade_hit(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(P, r, c, round - 1));
+            }
+        }
+    }
+}
+
+template <bool PRIMARY>
+__global__ __launch_bounds__(BLOCK) void k_trace(TraceParams P) {
+    const uint32_t shard = blockIdx.x % NSHARD;
+    uint32_t err = 0;
+    uint32_t shadow = 0;
+    if (PRIMARY) {
+        const int64_t n = P.n_primary;
+        for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
+            const int64_t i = base + threadIdx.x;
+            const bool active = i < n;
+            Ray r;
+            r.o = r.d = d3{0.0, 0.0, 0.0};
+            r.w = d3{1.0, 1.0, 1.0};
+            r.meta = pack_meta(0, 0, 0);
+            r.pix = 0; r.path = 0;
+            int s_local = 0;
+            if (active) {
+                s_local = (int)(i / P.npix);
+                uint32_t p = (uint32_t)(i - (int64_t)s_local * P.npix);
+                uint32_t lr = p / (uint32_t)P.cam.width;
+                uint32_t col = p - lr * (uint32_t)P.cam.width;
+                int grow = P.rows[lr];
+                double j[4];
+                primary_uniforms(P, s_local, p, (uint32_t)grow * (uint32_t)P.cam.width + col, j);
+                primary_ray(P.cam, P.cam.xs[col], P.cam.ys[grow], j, r.o, r.d);
+                r.pix = p;
+                r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s_local));
+            }
+            int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s_local * P.npix + r.pix : nullptr;
+            trace_one(P, r, active, shard, err, shadow, hs);
+        }
+    } else {
+        const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
+        const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
+        const int64_t off = (int64_t)shard * P.seg;
+        for (int64_t base = blk * BLOCK; base < n; base += nblk * BLOCK) {
+            const int64_t i = base + threadIdx.x;
+            const bool active = i < n;
+            Ray r;
+            if (active) {
+                r = queue_load(P.qin, off + i);
+            } else {
+                r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
+                r.pix = 0; r.meta = 0; r.path = 0;
+            }
+            trace_one(P, r, active, shard, err, shadow, nullptr);
+        }
+    }
+    if (err) atomicOr(&P.flags[0], err);
+    if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npix, double inv_spp_div, double spp,
+                                                  double* rgb, uint8_t* u8) {
+    for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK) {
+        double r = fb[p] / spp, g = fb[npix + p] / spp, b = fb[2 * npix + p] / spp;
+        uint8_t px[3];
+        double a0, a1, a2;
+        resolve_pixel(r, g, b, a0, a1, a2, px);
+        if (rgb) { rgb[p] = r; rgb[npix + p] = g; rgb[2 * npix + p] = b; }
+        if (u8) { u8[3 * p] = px[0]; u8[3 * p + 1] = px[1]; u8[3 * p + 2] = px[2]; }
+    }
+    (void)inv_spp_div;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O, const double* D, int64_t n, double* t,
+                                                  int32_t* id, double* orient) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        d3 o = d3{O[i], O[n + i], O[2 * n + i]}, d = d3{D[i], D[n + i], D[2 * n + i]};
+        double tn, on;
+        bool ties;
+        int c = nearest_hit(S, o, d, tn, on, ties);
+        if (t) t[i] = tn;
+        if (id) id[i] = c;
+        if (orient) orient[i] = on;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_intersect_one(srt_collider c, const double* O, const double* D, int64_t n,
+                                                        double* out) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        d3 o = d3{O[i], O[n + i], O[2 * n + i]}, d = d3{D[i], D[n + i], D[2 * n + i]};
+        double orient;
+        double t = collider_hit(c, o, d, orient);
+        out[i] = t;
+        out[n + i] = orient;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_primary_rays(srt_camera cam, const double* J, int64_t n, double* O,
+                                                       double* D) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        uint32_t row = (uint32_t)(i / cam.width), col = (uint32_t)(i - (int64_t)row * cam.width);
+        double j[4] = {J[i], J[n + i], J[2 * n + i], J[3 * n + i]};
+        d3 o, d;
+        primary_ray(cam, cam.xs[col], cam.ys[row], j, o, d);
+        O[i] = o.x; O[n + i] = o.y; O[2 * n + i] = o.z;
+        D[i] = d.x; D[n + i] = d.y; D[2 * n + i] = d.z;
+    }
+}
+
+template <typename T>
+hipError_t dalloc(T** p, int64_t count) {
+    return hipMalloc((void**)p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
+}
+
+int grid_for(int64_t n, int max_blocks) {
+    int64_t b = (n + BLOCK - 1) / BLOCK;
+    if (b < 1) b = 1;
+    return (int)std::min<int64_t>(b, max_blocks);
+}
+
+// seed the queue from caller rays (get_raycolor): ray i -> shard i % NSHARD, slot i / NSHARD
+__global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, const double* O, const double* D,
+                                                     const int32_t* med, int64_t n, uint32_t depth, uint32_t dfl) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        int64_t dst = (i % NSHARD) * seg + i / NSHARD;
+        queue_store(q, dst, d3{O[i], O[n + i], O[2 * n + i]}, d3{D[i], D[n + i], D[2 * n + i]}, d3{1.0, 1.0, 1.0},
+                    (uint32_t)i, pack_meta(med ? (uint32_t)med[i] : 0u, depth, dfl), mix32(0x7A11u, (uint32_t)i));
+    }
+}
+
+}  // namespace
+
+struct srt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int max_blocks = 2048;
+    int64_t queue_budget = (int64_t)96 << 30;  // bytes for both ray queues
+    // scene
+    bool has_scene = false;
+    SceneView S{};
+    int max_depth = 0;
+    int has_diffuse = 0;
+    int fanout = 1;
+    std::vector<void*> scene_bufs;
+    // ray queues: 2 x NSHARD segments of `seg` rays
+    Queue q[2]{};
+    int64_t seg = 0;
+    std::vector<void*> queue_bufs;
+    // frame
+    double* fb = nullptr;
+    int64_t fb_cap = 0;
+    double* rgb = nullptr;
+    int64_t rgb_cap = 0;
+    uint8_t* u8 = nullptr;
+    int64_t u8_cap = 0;
+    double* xs = nullptr;
+    double* ys = nullptr;
+    int32_t* rows = nullptr;
+    int64_t cam_cap[3] = {0, 0, 0};
+    double* jit = nullptr;
+    int64_t jit_cap = 0;
+    int32_t* hit = nullptr;
+    int64_t hit_cap = 0;
+    uint32_t* counts = nullptr;  // [SRT_MAX_DEPTHS][NSHARD]
+    uint32_t* flags = nullptr;   // [2]
+    unsigned long long* shadow = nullptr;
+    std::vector<hipEvent_t> ev;
+};
+
+namespace {
+
+void free_list(std::vector<void*>& v) {
+    for (void* p : v)
+        if (p) (void)hipFree(p);
+    v.clear();
+}
+
+// make room for `rays` queued rays per depth (spread over the shards with slack)
+int ensure_queues(srt_ctx* c, int64_t rays) {
+    int64_t seg = (rays + NSHARD - 1) / NSHARD;
+    seg = seg + seg / 8 + 1024;
+    if (seg <= c->seg) return SRT_OK;
+    free_list(c->queue_bufs);
+    c->seg = 0;
+    const int64_t n = seg * NSHARD;
+    for (int k = 0; k < 2; ++k) {
+        Queue& q = c->q[k];
+        double** dptr[9] = {&q.ox, &q.oy, &q.oz, &q.dx, &q.dy, &q.dz, &q.wr, &q.wg, &q.wb};
+        for (double** p : dptr) {
+            if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray queue allocation failed");
+            c->queue_bufs.push_back(*p);
+        }
+        uint32_t** uptr[3] = {&q.pix, &q.meta, &q.path};
+        for (uint32_t** p : uptr) {
+            if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray queue allocation failed");
+            c->queue_bufs.push_back(*p);
+        }
+    }
+    c->seg = seg;
+    return SRT_OK;
+}
+
+template <typename T>
+int ensure_buf(T** p, int64_t& cap, int64_t count) {
+    if (count <= cap && *p) return SRT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (dalloc(p, count) != hipSuccess) return fail(SRT_ERR_MEMORY, "device allocation failed");
+    cap = count;
+    return SRT_OK;
+}
+
+template <typename T>
+int upload(srt_ctx* c, const T* src, int64_t count, T** dst) {
+    *dst = nullptr;
+    if (count <= 0 || !src) return SRT_OK;
+    HIP_TRY(dalloc(dst, count));
+    c->scene_bufs.push_back(*dst);
+    HIP_TRY(hipMemcpy(*dst, src, (size_t)count * sizeof(T), hipMemcpyDefault));
+    return SRT_OK;
+}
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+int check_flags(uint32_t f0) {
+    if (f0 & ERR_INDEX)
+        return fail(SRT_ERR_INDEX, "index out of bounds in a texture/table lookup (reference raises IndexError)");
+    if (f0 & ERR_UNSUPPORTED) return fail(SRT_ERR_ARG, "uv requested on a Triangle (undefined in the reference)");
+    return SRT_OK;
+}
+
+TraceParams base_params(srt_ctx* c, uint64_t seed) {
+    TraceParams P{};
+    P.S = c->S;
+    P.flags = c->flags;
+    P.shadow = c->shadow;
+    P.seg = c->seg;
+    P.seed = seed;
+    return P;
+}
+
+// deepest depth index that can hold rays: max_ray_depth, +2 diffuse bounces without depth check
+int depth_cap(const srt_ctx* c) { return std::min(SRT_MAX_DEPTHS - 2, c->max_depth + 1 + (c->has_diffuse ? 2 : 0)); }
+
+int trace_grid(const srt_ctx* c) { return std::max(NSHARD, (c->max_blocks / NSHARD) * NSHARD); }
+
+int64_t depth_total(const uint32_t* cnt, int64_t seg) {
+    int64_t t = 0;
+    for (int s = 0; s < NSHARD; ++s) t += std::min<int64_t>(cnt[s], seg);
+    return t;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srt_abi_version(void) { return SRT_ABI_VERSION; }
+
+const char* srt_last_error(void) { return g_err.c_str(); }
+
+int srt_device_count(int* count) {
+    if (!count) return fail(SRT_ERR_ARG, "count is null");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(SRT_ERR_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *count = n;
+    return SRT_OK;
+}
+
+int srt_create(int device, srt_ctx** out) {
+    if (!out) return fail(SRT_ERR_ARG, "out is null");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    srt_ctx* c = new srt_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    c->max_blocks = prop.multiProcessorCount * 8;
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(dalloc(&c->counts, SRT_MAX_DEPTHS * NSHARD));
+    HIP_TRY(dalloc(&c->flags, 2));
+    HIP_TRY(dalloc(&c->shadow, 1));
+    *out = c;
+    return SRT_OK;
+}
+
+int srt_destroy(srt_ctx* c) {
+    if (!c) return SRT_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_list(c->scene_bufs);
+    free_list(c->queue_bufs);
+    void* bufs[] = {c->fb, c->rgb, c->u8, c->xs, c->ys, c->rows, c->jit, c->hit, c->counts, c->flags, c->shadow};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SRT_OK;
+}
+
+int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
+    if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
+    if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
+    if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
+    return fail(SRT_ERR_ARG, std::string("unknown option ") + key);
+}
+
+int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
+    if (!c || !d) return fail(SRT_ERR_ARG, "null ctx/scene");
+    if (d->n_colliders < 0 || d->n_materials < 0 || d->n_media < 1 || d->n_media > 255)
+        return fail(SRT_ERR_ARG, "scene needs 1 <= n_media <= 255 (row 0 = scene.n)");
+    for (int i = 0; i < d->n_colliders; ++i) {
+        const srt_collider& cc = d->colliders[i];
+        if (cc.type < 0 || cc.type > 3) return fail(SRT_ERR_ARG, "bad collider type");
+        if (cc.material < 0 || cc.material >= d->n_materials) return fail(SRT_ERR_ARG, "collider material out of range");
+    }
+    for (int i = 0; i < d->n_materials; ++i) {
+        const srt_material& m = d->materials[i];
+        int texs[4] = {m.tex, m.tex_aux0, m.tex_aux1, m.normalmap};
+        for (int t : texs)
+            if (t >= d->n_textures) return fail(SRT_ERR_ARG, "material texture index out of range");
+        if (m.type == SRT_REFRACTIVE && (m.medium < 0 || m.medium >= d->n_media))
+            return fail(SRT_ERR_ARG, "refractive medium out of range");
+        if ((m.type == SRT_SKY && m.tex < 0) || (m.type == SRT_THINFILM && (m.tex_aux0 < 0 || m.tex_aux1 < 0)))
+            return fail(SRT_ERR_ARG, "material is missing a required texture");
+        if (m.type == SRT_DIFFUSE && (m.ival < 1 || m.ival > 255)) return fail(SRT_ERR_ARG, "diffuse_rays must be 1..255");
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    free_list(c->scene_bufs);
+    c->has_scene = false;
+    SceneView S{};
+    int rc;
+    srt_collider* col;
+    srt_material* mat;
+    srt_texture* tex;
+    uint8_t* texels;
+    srt_light* lights;
+    double *media, *f0, *ll, *imp;
+    if ((rc = upload(c, d->colliders, d->n_colliders, &col))) return rc;
+    if ((rc = upload(c, d->materials, d->n_materials, &mat))) return rc;
+    if ((rc = upload(c, d->textures, d->n_textures, &tex))) return rc;
+    if ((rc = upload(c, d->texels, d->texel_bytes, &texels))) return rc;
+    if ((rc = upload(c, d->lights, d->n_lights, &lights))) return rc;
+    if ((rc = upload(c, d->media, (int64_t)d->n_media * 6, &media))) return rc;
+    if ((rc = upload(c, d->glossy_f0, (int64_t)d->n_materials * d->n_media * 3, &f0))) return rc;
+    if ((rc = upload(c, d->light_local, (int64_t)d->n_lights * d->n_colliders * 3, &ll))) return rc;
+    if ((rc = upload(c, d->importance, (int64_t)d->n_importance * 4, &imp))) return rc;
+    S.col = col; S.mat = mat; S.tex = tex; S.texels = texels; S.lights = lights;
+    S.media = media; S.glossy_f0 = f0; S.light_local = ll; S.importance = imp;
+    S.ncol = d->n_colliders; S.nmat = d->n_materials; S.ntex = d->n_textures; S.nlights = d->n_lights;
+    S.nmedia = d->n_media; S.nimp = d->n_importance;
+    S.nshadow = 0;
+    int fan = 1;
+    c->has_diffuse = 0;
+    for (int i = 0; i < d->n_colliders; ++i)
+        if (d->colliders[i].flags & SRT_CF_SHADOW) S.nshadow++;
+    for (int i = 0; i < d->n_materials; ++i) {
+        const srt_material& m = d->materials[i];
+        if (m.type == SRT_REFRACTIVE || m.type == SRT_THINFILM) fan = std::max(fan, 2);
+        if (m.type == SRT_DIFFUSE) { fan = std::max(fan, std::max(1, (int)m.ival)); c->has_diffuse = 1; }
+    }
+    for (int k = 0; k < 3; ++k) S.ambient[k] = d->ambient[k];
+    c->S = S;
+    c->max_depth = std::max(0, (int)d->max_ray_depth);
+    c->fanout = fan;
+    c->has_scene = true;
+    return SRT_OK;
+}
+
+int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
+    auto t_start = std::chrono::steady_clock::now();
+    if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
+    if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
+    if (a->spp <= 0 || cam->width <= 0 || cam->height <= 0 || a->n_rows <= 0 || !cam->xs || !cam->ys)
+        return fail(SRT_ERR_ARG, "spp, width, height, n_rows must be positive and xs/ys set");
+    std::vector<int32_t> rows_h;
+    if (a->rows) {
+        if (is_device_ptr(a->rows)) return fail(SRT_ERR_ARG, "rows must be host memory");
+        for (int k = 0; k < a->n_rows; ++k)
+            if (a->rows[k] < 0 || a->rows[k] >= cam->height) return fail(SRT_ERR_ARG, "row index out of range");
+    } else {
+        if (a->n_rows > cam->height) return fail(SRT_ERR_ARG, "n_rows > height");
+        rows_h.resize(a->n_rows);
+        for (int k = 0; k < a->n_rows; ++k) rows_h[k] = k;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t W = cam->width;
+    const int64_t npix = (int64_t)a->n_rows * W;
+    if (npix >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "image too large");
+    int rc;
+    if ((rc = ensure_buf(&c->xs, c->cam_cap[0], W))) return rc;
+    if ((rc = ensure_buf(&c->ys, c->cam_cap[1], cam->height))) return rc;
+    if ((rc = ensure_buf(&c->rows, c->cam_cap[2], a->n_rows))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->xs, cam->xs, W * 8, hipMemcpyDefault, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->ys, cam->ys, (size_t)cam->height * 8, hipMemcpyDefault, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->rows, a->rows ? a->rows : rows_h.data(), (size_t)a->n_rows * 4, hipMemcpyDefault,
+                           c->stream));
+    if ((rc = ensure_buf(&c->fb, c->fb_cap, 3 * npix))) return rc;
+    if ((rc = ensure_buf(&c->rgb, c->rgb_cap, 3 * npix))) return rc;
+    if ((rc = ensure_buf(&c->u8, c->u8_cap, 3 * npix))) return rc;
+    // samples per pass: both queues must hold spp_pass * npix * fanout rays
+    const int64_t per_sample = npix * c->fanout;
+    const int64_t budget_rays = c->queue_budget / (2 * RAY_BYTES);
+    int batch = a->batch_spp > 0 ? a->batch_spp
+                                 : (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, budget_rays / per_sample));
+    batch = std::min(batch, a->spp);
+    while (batch > 1 && (int64_t)batch * npix * c->fanout >= ((int64_t)1 << 32) - 1) batch /= 2;
+    const bool jit_dev = is_device_ptr(a->jitter);
+    if (a->jitter && !jit_dev && (rc = ensure_buf(&c->jit, c->jit_cap, (int64_t)batch * 4 * npix))) return rc;
+    const bool hit_dev = is_device_ptr(a->out_hit_id);
+    if (a->out_hit_id && !hit_dev && (rc = ensure_buf(&c->hit, c->hit_cap, (int64_t)batch * npix))) return rc;
+    const int dcap = depth_cap(c);
+    if ((int)c->ev.size() < dcap + 2) {
+        for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+        c->ev.assign(dcap + 2, nullptr);
+        for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+    }
+    if ((rc = ensure_queues(c, (int64_t)batch * npix * c->fanout))) return rc;
+    srt_stats S{};
+    HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * npix * 8, c->stream));
+    HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
+    double ms_trace = 0.0, ms_primary = 0.0, ms_device = 0.0;
+    std::vector<uint32_t> counts(SRT_MAX_DEPTHS * NSHARD);
+    for (int s0 = 0; s0 < a->spp;) {
+        const int ns = std::min(batch, a->spp - s0);
+        const int64_t nrays = (int64_t)ns * npix;
+        HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->stream));
+        HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
+        TraceParams P = base_params(c, a->seed);
+        P.fb = c->fb;
+        P.npix = npix;
+        P.cam = *cam;
+        P.cam.xs = c->xs;
+        P.cam.ys = c->ys;
+        P.rows = c->rows;
+        P.sample_base = a->sample_base + s0;
+        if (a->jitter) {
+            const double* src = a->jitter + (int64_t)s0 * 4 * npix;
+            if (jit_dev) {
+                P.jitter = src;
+            } else {
+                HIP_TRY(hipMemcpyAsync(c->jit, src, (size_t)nrays * 4 * 8, hipMemcpyHostToDevice, c->stream));
+                P.jitter = c->jit;
+            }
+        }
+        if (a->out_hit_id) P.hit_out = hit_dev ? a->out_hit_id + (int64_t)s0 * npix : c->hit;
+        // depth 0: raygen fused with the trace step
+        P.depth = 0;
+        P.n_primary = nrays;
+        P.qout = c->q[1];
+        P.cnt_out = c->counts + NSHARD;
+        HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+        hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(nrays, c->max_blocks)), dim3(BLOCK), 0, c->stream, P);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+        for (int d = 1; d <= dcap; ++d) {
+            P.depth = d;
+            P.qin = c->q[d & 1];
+            P.qout = c->q[(d + 1) & 1];
+            P.cnt_in = c->counts + (int64_t)d * NSHARD;
+            P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
+            hipLaunchKernelGGL(k_trace<false>, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(c->ev[1 + d], c->stream));
+        }
+        uint32_t flags[2];
+        HIP_TRY(hipMemcpyAsync(counts.data(), c->counts, counts.size() * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(flags, c->flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+        if (a->out_hit_id && !hit_dev)
+            HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->hit, (size_t)nrays * 4,
+                                   hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((rc = check_flags(flags[0]))) return rc;
+        if (flags[1]) {
+            // a queue shard overflowed: grow and restart the frame (this pass's sum is partial)
+            S.retries++;
+            if (S.retries > 8) return fail(SRT_ERR_MEMORY, "ray queues keep overflowing");
+            if ((rc = ensure_queues(c, 2 * c->seg * NSHARD))) return rc;
+            HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * npix * 8, c->stream));
+            HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
+            s0 = 0;
+            for (auto& v : S.rays_per_depth) v = 0;
+            ms_trace = ms_primary = ms_device = 0.0;
+            S.passes = 0;
+            continue;
+        }
+        if (depth_total(counts.data() + (int64_t)(dcap + 1) * NSHARD, c->seg) != 0)
+            return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
+        S.rays_per_depth[0] += nrays;
+        for (int d = 1; d <= dcap; ++d) S.rays_per_depth[d] += depth_total(counts.data() + (int64_t)d * NSHARD, c->seg);
+        float ms;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        ms_primary += ms;
+        ms_trace += ms;
+        for (int d = 1; d <= dcap; ++d) {
+            HIP_TRY(hipEventElapsedTime(&ms, c->ev[d], c->ev[d + 1]));
+            ms_trace += ms;
+        }
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[dcap + 1]));
+        ms_device += ms;
+        S.passes++;
+        s0 += ns;
+    }
+    hipLaunchKernelGGL(k_resolve, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb, npix, 0.0,
+                       (double)a->spp, c->rgb, c->u8);
+    HIP_TRY(hipGetLastError());
+    if (a->out_rgb)
+        HIP_TRY(hipMemcpyAsync(a->out_rgb, c->rgb, (size_t)3 * npix * 8, hipMemcpyDefault, c->stream));
+    if (a->out_srgb8) HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->u8, (size_t)3 * npix, hipMemcpyDefault, c->stream));
+    unsigned long long shadow = 0;
+    HIP_TRY(hipMemcpyAsync(&shadow, c->shadow, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (st) {
+        S.n_depths = dcap + 1;
+        S.total_rays = 0;
+        for (int d = 0; d <= dcap; ++d) S.total_rays += S.rays_per_depth[d];
+        S.shadow_rays = (int64_t)shadow;
+        S.ms_trace_kernels = ms_trace;
+        S.ms_primary_kernel = ms_primary;
+        S.ms_device = ms_device;
+        S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        *st = S;
+    }
+    return SRT_OK;
+}
+
+int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
+    auto t_start = std::chrono::steady_clock::now();
+    if (!c || !a || !a->origin || !a->dir || !a->out_rgb) return fail(SRT_ERR_ARG, "null argument");
+    if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
+    if (a->depth < 0 || a->depth > 200 || a->diffuse_reflections < 0) return fail(SRT_ERR_ARG, "bad depth");
+    if (a->n <= 0) return SRT_OK;
+    if (a->n >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "batch too large");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t n = a->n;
+    int rc = SRT_OK;
+    double *O = nullptr, *D = nullptr;
+    int32_t* med = nullptr;
+    HIP_TRY(dalloc(&O, 3 * n));
+    HIP_TRY(dalloc(&D, 3 * n));
+    if (a->medium) HIP_TRY(dalloc(&med, n));
+    HIP_TRY(hipMemcpyAsync(O, a->origin, (size_t)3 * n * 8, hipMemcpyDefault, c->stream));
+    HIP_TRY(hipMemcpyAsync(D, a->dir, (size_t)3 * n * 8, hipMemcpyDefault, c->stream));
+    if (med) HIP_TRY(hipMemcpyAsync(med, a->medium, (size_t)n * 4, hipMemcpyDefault, c->stream));
+    if ((rc = ensure_buf(&c->fb, c->fb_cap, 3 * n))) return rc;
+    if ((rc = ensure_queues(c, n * c->fanout))) return rc;
+    // depths a->depth .. a->depth + cap (the batch's depth is a scalar in the reference)
+    const int d0 = a->depth;
+    const int dlast = std::min(SRT_MAX_DEPTHS - 2, d0 + depth_cap(c));
+    srt_stats S{};
+    std::vector<uint32_t> counts(SRT_MAX_DEPTHS * NSHARD);
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 8) { rc = fail(SRT_ERR_MEMORY, "ray queues keep overflowing"); break; }
+        HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * n * 8, c->stream));
+        HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->stream));
+        HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
+        HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
+        uint32_t seed_counts[NSHARD];
+        for (int s = 0; s < NSHARD; ++s) seed_counts[s] = (uint32_t)((n - s + NSHARD - 1) / NSHARD);
+        HIP_TRY(hipMemcpyAsync(c->counts + (int64_t)d0 * NSHARD, seed_counts, sizeof(seed_counts),
+                               hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_seed_queue, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->q[d0 & 1],
+                           c->seg, O, D, med, n, (uint32_t)d0, (uint32_t)a->diffuse_reflections);
+        HIP_TRY(hipGetLastError());
+        TraceParams P = base_params(c, a->seed);
+        P.fb = c->fb;
+        P.npix = n;
+        for (int d = d0; d <= dlast; ++d) {
+            P.depth = d;
+            P.qin = c->q[d & 1];
+            P.qout = c->q[(d + 1) & 1];
+            P.cnt_in = c->counts + (int64_t)d * NSHARD;
+            P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
+            hipLaunchKernelGGL(k_trace<false>, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
+            HIP_TRY(hipGetLastError());
+        }
+        uint32_t flags[2];
+        unsigned long long shadow = 0;
+        HIP_TRY(hipMemcpyAsync(counts.data(), c->counts, counts.size() * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(flags, c->flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&shadow, c->shadow, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((rc = check_flags(flags[0]))) break;
+        if (flags[1]) {
+            S.retries++;
+            if ((rc = ensure_queues(c, 2 * c->seg * NSHARD))) break;
+            continue;
+        }
+        if (depth_total(counts.data() + (int64_t)(dlast + 1) * NSHARD, c->seg) != 0) {
+            rc = fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
+            break;
+        }
+        for (int d = d0; d <= dlast; ++d) S.rays_per_depth[d] = depth_total(counts.data() + (int64_t)d * NSHARD, c->seg);
+        S.n_depths = dlast + 1;
+        for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.total_rays += S.rays_per_depth[d];
+        S.shadow_rays = (int64_t)shadow;
+        HIP_TRY(hipMemcpy(a->out_rgb, c->fb, (size_t)3 * n * 8, hipMemcpyDefault));
+        break;
+    }
+    (void)hipFree(O);
+    (void)hipFree(D);
+    if (med) (void)hipFree(med);
+    if (rc) return rc;
+    S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (st) *st = S;
+    return SRT_OK;
+}
+
+int srt_nearest(srt_ctx* c, const double* O, const double* D, int64_t n, double* t, int32_t* id, double* orient) {
+    if (!c || !O || !D) return fail(SRT_ERR_ARG, "null argument");
+    if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
+    if (n <= 0) return SRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    double *dO, *dD, *dt, *dor;
+    int32_t* did;
+    HIP_TRY(dalloc(&dO, 3 * n));
+    HIP_TRY(dalloc(&dD, 3 * n));
+    HIP_TRY(dalloc(&dt, n));
+    HIP_TRY(dalloc(&dor, n));
+    HIP_TRY(dalloc(&did, n));
+    HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
+    hipLaunchKernelGGL(k_nearest, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->S, dO, dD, n, dt, did,
+                       dor);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (t) HIP_TRY(hipMemcpy(t, dt, (size_t)n * 8, hipMemcpyDefault));
+    if (id) HIP_TRY(hipMemcpy(id, did, (size_t)n * 4, hipMemcpyDefault));
+    if (orient) HIP_TRY(hipMemcpy(orient, dor, (size_t)n * 8, hipMemcpyDefault));
+    void* bufs[] = {dO, dD, dt, dor, did};
+    for (void* p : bufs) (void)hipFree(p);
+    return SRT_OK;
+}
+
+int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O, const double* D, int64_t n,
+                           double* out) {
+    if (!c || !col || !O || !D || !out) return fail(SRT_ERR_ARG, "null argument");
+    if (col->type < 0 || col->type > 3) return fail(SRT_ERR_ARG, "bad collider type");
+    if (n <= 0) return SRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    double *dO, *dD, *dout;
+    HIP_TRY(dalloc(&dO, 3 * n));
+    HIP_TRY(dalloc(&dD, 3 * n));
+    HIP_TRY(dalloc(&dout, 2 * n));
+    HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
+    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, *col, dO, dD, n,
+                       dout);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(out, dout, (size_t)2 * n * 8, hipMemcpyDefault));
+    (void)hipFree(dO);
+    (void)hipFree(dD);
+    (void)hipFree(dout);
+    return SRT_OK;
+}
+
+int srt_primary_rays(srt_ctx* c, const srt_camera* cam, const double* J, double* O, double* D) {
+    if (!c || !cam || !J || !O || !D) return fail(SRT_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t n = (int64_t)cam->width * cam->height;
+    double *dJ, *dO, *dD, *xs, *ys;
+    HIP_TRY(dalloc(&dJ, 4 * n));
+    HIP_TRY(dalloc(&dO, 3 * n));
+    HIP_TRY(dalloc(&dD, 3 * n));
+    HIP_TRY(dalloc(&xs, cam->width));
+    HIP_TRY(dalloc(&ys, cam->height));
+    HIP_TRY(hipMemcpy(dJ, J, (size_t)4 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(xs, cam->xs, (size_t)cam->width * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(ys, cam->ys, (size_t)cam->height * 8, hipMemcpyDefault));
+    srt_camera k = *cam;
+    k.xs = xs;
+    k.ys = ys;
+    hipLaunchKernelGGL(k_primary_rays, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, k, dJ, n, dO, dD);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(O, dO, (size_t)3 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(D, dD, (size_t)3 * n * 8, hipMemcpyDefault));
+    void* bufs[] = {dJ, dO, dD, xs, ys};
+    for (void* p : bufs) (void)hipFree(p);
+    return SRT_OK;
+}
+
+int srt_device_alloc(srt_ctx* c, int64_t bytes, void** out) {
+    if (!c || !out || bytes <= 0) return fail(SRT_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMalloc(out, (size_t)bytes));
+    return SRT_OK;
+}
+
+int srt_device_free(srt_ctx* c, void* p) {
+    if (!c) return fail(SRT_ERR_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    if (p) HIP_TRY(hipFree(p));
+    return SRT_OK;
+}
+
+int srt_memcpy(srt_ctx* c, void* dst, const void* src, int64_t bytes) {
+    if (!c || !dst || !src || bytes < 0) return fail(SRT_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault));
+    return SRT_OK;
+}
+
+int srt_synchronize(srt_ctx* c) {
+    if (!c) return fail(SRT_ERR_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return SRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,174 @@
+"""Device backend: one libsightpy_hip.so context per process, scene upload cache, entry points used
+by the public API (Scene.render, get_raycolor, get_distances, Collider.intersect, Camera.get_ray).
+
+There is deliberately no CPU path here: if the HIP library or a GPU is missing every entry point
+raises `BackendUnavailable`.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _native as N
+from ._lower import lower_scene, camera_desc, collider_record
+from .utils.vector3 import vec3
+
+_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": None}
+
+
+class RenderResult:
+    def __init__(self, srgb8, rgb, hit_ids, stats):
+        self.srgb8 = srgb8
+        self.rgb = rgb
+        self.hit_ids = hit_ids
+        self.stats = stats
+
+
+def library():
+    if _STATE["lib"] is None:
+        _STATE["lib"] = N.load_library()
+    return _STATE["lib"]
+
+
+def context():
+    """The process's device context (device = $SIGHTPY_DEVICE, else $LOCAL_RANK, else 0)."""
+    if _STATE["ctx"] is None:
+        lib = library()
+        n = ctypes.c_int(0)
+        rc = lib.srt_device_count(ctypes.byref(n))
+        if rc != 0 or n.value < 1:
+            raise N.BackendUnavailable(
+                "no HIP device visible (%s); sightpy on MI355X has no CPU fallback"
+                % lib.srt_last_error().decode(errors="replace")
+            )
+        dev = int(os.environ.get("SIGHTPY_DEVICE", os.environ.get("LOCAL_RANK", "0"))) % n.value
+        ctx = ctypes.c_void_p()
+        N.check(lib, lib.srt_create(dev, ctypes.byref(ctx)))
+        _STATE["ctx"] = ctx
+        _STATE["device"] = dev
+    return _STATE["lib"], _STATE["ctx"]
+
+
+def upload(scene, extra_media=(), force=False):
+    """Lower and upload `scene` unless the identical tables are already resident."""
+    lib, ctx = context()
+    L = lower_scene(scene, extra_media)
+    sig = L.signature()
+    if force or sig != _STATE["scene_sig"]:
+        _STATE["scene_sig"] = None
+        N.check(lib, lib.srt_upload_scene(ctx, ctypes.byref(L.desc())))
+        _STATE["scene_sig"] = sig
+    return L
+
+
+def _planar(v, n=None):
+    """vec3 (scalars or arrays) -> C-contiguous float64 (3, n)."""
+    comps = [np.asarray(c, dtype=np.float64) for c in (v.x, v.y, v.z)]
+    if n is None:
+        n = max([c.size for c in comps])
+    return np.ascontiguousarray(np.stack([np.broadcast_to(c.reshape(-1) if c.ndim else c, (n,)) for c in comps]))
+
+
+def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False):
+    """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG."""
+    lib, ctx = context()
+    upload(scene)
+    cam = scene.camera
+    W, H = int(cam.screen_width), int(cam.screen_height)
+    rows_arr = None if rows is None else np.ascontiguousarray(rows, dtype=np.int32)
+    nrows = H if rows_arr is None else len(rows_arr)
+    npix = nrows * W
+    cd = camera_desc(cam)
+    a = N.RenderArgs()
+    a.spp = int(spp)
+    a.sample_base = 0
+    a.n_rows = nrows
+    a.batch_spp = int(batch_size or 0)
+    a.rows = N.ptr(rows_arr)
+    j = None
+    if jitter is not None:
+        j = np.ascontiguousarray(jitter, dtype=np.float64)
+        if j.shape != (spp, 4, npix):
+            raise ValueError("jitter must have shape (spp, 4, %d)" % npix)
+        a.jitter = N.ptr(j)
+    a.seed = int(seed if seed is not None else np.random.randint(0, 2**63 - 1, dtype=np.int64)) & (2**64 - 1)
+    rgb = np.empty((3, npix)) if want_rgb else None
+    u8 = np.empty((npix, 3), dtype=np.uint8)
+    hits = np.empty((spp, npix), dtype=np.int32) if want_hits else None
+    a.out_rgb = N.ptr(rgb)
+    a.out_srgb8 = N.ptr(u8)
+    a.out_hit_id = N.ptr(hits)
+    st = N.Stats()
+    N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
+    return RenderResult(u8.reshape(nrows, W, 3), rgb, hits, st.as_dict())
+
+
+def _media_of(ray_n, count):
+    """Per-ray complex IOR triples -> (unique triples, index per ray)."""
+    comps = [np.asarray(c) for c in (ray_n.x, ray_n.y, ray_n.z)]
+    cols = [np.broadcast_to(c.astype(np.complex128), (count,)) for c in comps]
+    tri = np.stack(cols, axis=1)
+    uniq, inv = np.unique(tri, axis=0, return_inverse=True)
+    return [tuple(complex(v) for v in row) for row in uniq], inv.reshape(-1).astype(np.int32)
+
+
+def trace_rays(ray, scene, seed=None, return_stats=False):
+    """get_raycolor(ray, scene) on the device: colour of every ray of the batch."""
+    lib, ctx = context()
+    n = len(ray)
+    uniq, inv = _media_of(ray.n, n)
+    L = upload(scene, extra_media=uniq)
+    remap = np.array([L.media_keys.index(k) for k in uniq], dtype=np.int32)
+    med = np.ascontiguousarray(remap[inv])
+    O = _planar(ray.origin, n)
+    D = _planar(ray.dir, n)
+    out = np.empty((3, n))
+    a = N.TraceArgs()
+    a.n = n
+    a.origin, a.dir, a.medium = N.ptr(O), N.ptr(D), N.ptr(med)
+    a.depth = int(ray.depth)
+    a.diffuse_reflections = int(ray.diffuse_reflections)
+    a.seed = int(seed if seed is not None else np.random.randint(0, 2**63 - 1, dtype=np.int64))
+    a.out_rgb = N.ptr(out)
+    st = N.Stats()
+    N.check(lib, lib.srt_trace(ctx, ctypes.byref(a), ctypes.byref(st)))
+    col = vec3(out[0], out[1], out[2])
+    return (col, st.as_dict()) if return_stats else col
+
+
+def nearest_hits(scene, O, D):
+    """Nearest hit over scene.collider_list: (t, collider index or -1, orientation)."""
+    lib, ctx = context()
+    upload(scene)
+    Oa = _planar(O)
+    n = Oa.shape[1]
+    Da = _planar(D, n)
+    t = np.empty(n)
+    ids = np.empty(n, dtype=np.int32)
+    orient = np.empty(n)
+    N.check(lib, lib.srt_nearest(ctx, N.ptr(Oa), N.ptr(Da), n, N.ptr(t), N.ptr(ids), N.ptr(orient)))
+    return t, ids, orient
+
+
+def intersect_collider(collider, O, D):
+    """Collider.intersect(O, D) -> (2, N) [distance; orientation] on the device."""
+    lib, ctx = context()
+    rec = np.ascontiguousarray(collider_record(collider))
+    Oa = _planar(O)
+    n = Oa.shape[1]
+    Da = _planar(D, n)
+    out = np.empty((2, n))
+    N.check(lib, lib.srt_intersect_collider(ctx, N.ptr(rec.reshape(1)), N.ptr(Oa), N.ptr(Da), n, N.ptr(out)))
+    return out
+
+
+def primary_rays(camera, jitter):
+    """Camera.get_ray geometry for one sample; jitter (4, H*W).  Returns (origin, dir) vec3."""
+    lib, ctx = context()
+    cd = camera_desc(camera)
+    n = int(camera.screen_width) * int(camera.screen_height)
+    J = np.ascontiguousarray(jitter, dtype=np.float64).reshape(4, n)
+    O = np.empty((3, n))
+    D = np.empty((3, n))
+    N.check(lib, lib.srt_primary_rays(ctx, ctypes.byref(cd), N.ptr(J), N.ptr(O), N.ptr(D)))
+    return vec3(O[0], O[1], O[2]), vec3(D[0], D[1], D[2])

@@ -1,0 +1,110 @@
+"""Scene assembly and the render entry point (reference `sightpy/scene.py:28-166`).
+
+`Scene` keeps the reference's assembly API.  `render()` is the drop-in boundary: instead of the
+reference's `multiprocessing.Pool` over samples (scene.py:80-116) it lowers the scene to flat
+device tables once, uploads the camera jitter drawn from numpy's global RNG in the reference's
+order (so a seeded render consumes the same random stream), and runs the whole
+samples x depths wavefront plus the sRGB resolve on the GPU through `libsightpy_hip.so`.
+"""
+import time
+
+import numpy as np
+from PIL import Image
+
+from .camera import Camera
+from .utils.constants import *
+from .utils.vector3 import vec3, rgb
+from . import lights
+from .backgrounds.skybox import SkyBox
+from .backgrounds.panorama import Panorama
+
+__all__ = ["Scene"]
+
+
+class Scene:
+    def __init__(self, ambient_color=rgb(0.01, 0.01, 0.01), n=vec3(1.0, 1.0, 1.0)):
+        self.scene_primitives = []
+        self.collider_list = []
+        self.shadowed_collider_list = []
+        self.Light_list = []
+        self.importance_sampled_list = []
+        self.ambient_color = ambient_color
+        self.n = n
+        self.last_stats = None
+
+    def add_Camera(self, look_from, look_at, **kwargs):
+        self.camera = Camera(look_from, look_at, **kwargs)
+
+    def add_PointLight(self, pos, color):
+        self.Light_list += [lights.PointLight(pos, color)]
+
+    def add_DirectionalLight(self, Ldir, color):
+        self.Light_list += [lights.DirectionalLight(Ldir.normalize(), color)]
+
+    def add(self, primitive, importance_sampled=False):
+        self.scene_primitives += [primitive]
+        self.collider_list += primitive.collider_list
+        if importance_sampled == True:
+            self.importance_sampled_list += [primitive]
+        if primitive.shadow == True:
+            self.shadowed_collider_list += primitive.collider_list
+
+    def add_Background(self, img, light_intensity=0.0, blur=0.0, spherical=False):
+        if spherical == False:
+            primitive = SkyBox(img, light_intensity=light_intensity, blur=blur)
+        else:
+            primitive = Panorama(img, light_intensity=light_intensity, blur=blur)
+        self.scene_primitives += [primitive]
+        self.collider_list += primitive.collider_list
+
+    def render(self, samples_per_pixel, progress_bar=False, batch_size=None, rng="numpy", seed=None):
+        """Render `samples_per_pixel` samples and return a PIL RGB image.
+
+        rng="numpy" (default) draws the primary-ray jitter from numpy's global legacy RNG exactly
+        as the reference does (including the extra sizing draw at scene.py:81), so seeded renders
+        match the reference.  rng="device" generates it on the GPU (Philox keyed by pixel and
+        sample).  `batch_size` bounds the samples traced per device pass (HBM budget).
+        """
+        from ._backend import render_scene
+
+        print("Rendering...")
+        t0 = time.time()
+        jitter = None
+        if rng == "numpy":
+            jitter = self.camera.draw_jitter(samples_per_pixel)
+            self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
+        elif rng != "device":
+            raise ValueError("rng must be 'numpy' or 'device'")
+        out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size)
+        self.last_stats = out.stats
+        print("Render Took", time.time() - t0)
+        return Image.fromarray(out.srgb8, "RGB")
+
+    def get_distances(self):
+        """Grey depth map of one primary sample (reference scene.py:142-166)."""
+        from ._backend import primary_rays, nearest_hits
+
+        print("Rendering...")
+        t0 = time.time()
+        jitter = self.camera.draw_jitter(1)[0]
+        O, D = primary_rays(self.camera, jitter)
+        t, _, _ = nearest_hits(self, O, D)
+        g = np.where(t <= 10, t, 10) / 10
+        print("Render Took", time.time() - t0)
+        h, w = self.camera.screen_height, self.camera.screen_width
+        u8 = (255 * np.clip(g, 0, 1).reshape((h, w))).astype(np.uint8)
+        return Image.fromarray(np.stack([u8, u8, u8], axis=-1), "RGB")
+
+
+def get_raycolor_tuple(x):
+    """Reference scene.py:16-17 (Pool worker shim); kept for API compatibility."""
+    from .ray import get_raycolor
+
+    return get_raycolor(*x)
+
+
+def batch_rays(rays, batch_size):
+    """Reference scene.py:20-25: concatenate per-sample Ray batches in groups of batch_size."""
+    from .ray import Ray
+
+    return [Ray.concatenate(rays[i:i + batch_size]) for i in range(0, len(rays), batch_size)]

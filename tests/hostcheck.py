@@ -1,0 +1,70 @@
+"""Loader for the test-only host check harness (python-raytracer_amd/csrc/rt_hostcheck.cpp):
+the kernels' per-ray functions compiled for the CPU, driven sequentially.  Used by the CPU test
+suite to check the device math and the scene lowering against the oracle without a GPU."""
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+from sightpy import _native as N
+from sightpy._lower import lower_scene, camera_desc, collider_record
+
+LIB = Path(__file__).resolve().parent / "_build" / "libsightpy_hostcheck.so"
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            import subprocess
+            subprocess.run(["make", "-C", str(Path(__file__).resolve().parent.parent / "python-raytracer_amd" / "csrc"),
+                            str(LIB.relative_to(LIB.parent.parent.parent).as_posix()).replace("tests/", "../../tests/")],
+                           check=True)
+        _lib = ctypes.CDLL(str(LIB))
+        _lib.hc_render.argtypes = [ctypes.POINTER(N.SceneDesc), ctypes.POINTER(N.CameraDesc),
+                                   ctypes.POINTER(N.RenderArgs), ctypes.POINTER(N.Stats)]
+        _lib.hc_trace.argtypes = [ctypes.POINTER(N.SceneDesc), ctypes.POINTER(N.TraceArgs), ctypes.POINTER(N.Stats)]
+        _lib.hc_nearest.argtypes = [ctypes.POINTER(N.SceneDesc)] + [ctypes.c_void_p] * 2 + [ctypes.c_int64] + \
+                                   [ctypes.c_void_p] * 3
+        _lib.hc_intersect_collider.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p]
+        _lib.hc_primary_rays.argtypes = [ctypes.POINTER(N.CameraDesc)] + [ctypes.c_void_p] * 3
+        _lib.hc_last_error.restype = ctypes.c_char_p
+    return _lib
+
+
+def render(scene, jitter, seed=0, rows=None):
+    L = lower_scene(scene)
+    d = L.desc()
+    cd = camera_desc(scene.camera)
+    spp = jitter.shape[0] if jitter is not None else 1
+    nrows = scene.camera.screen_height if rows is None else len(rows)
+    npix = nrows * scene.camera.screen_width
+    a = N.RenderArgs()
+    a.spp = spp
+    a.n_rows = nrows
+    rows_arr = None if rows is None else np.ascontiguousarray(rows, dtype=np.int32)
+    a.rows = N.ptr(rows_arr)
+    j = None if jitter is None else np.ascontiguousarray(jitter)
+    a.jitter = N.ptr(j)
+    a.seed = seed
+    rgb = np.empty((3, npix))
+    u8 = np.empty((npix, 3), np.uint8)
+    hits = np.empty((spp, npix), np.int32)
+    a.out_rgb, a.out_srgb8, a.out_hit_id = N.ptr(rgb), N.ptr(u8), N.ptr(hits)
+    st = N.Stats()
+    rc = lib().hc_render(ctypes.byref(d), ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st))
+    if rc:
+        if rc == N.ERR_INDEX:
+            raise IndexError(lib().hc_last_error().decode())
+        raise RuntimeError(lib().hc_last_error().decode())
+    return rgb, u8.reshape(nrows, scene.camera.screen_width, 3), hits, st.as_dict()
+
+
+def intersect(collider, O, D):
+    rec = np.ascontiguousarray(collider_record(collider)).reshape(1)
+    O = np.ascontiguousarray(O, dtype=np.float64)
+    D = np.ascontiguousarray(D, dtype=np.float64)
+    out = np.empty((2, O.shape[1]))
+    lib().hc_intersect_collider(N.ptr(rec), N.ptr(O), N.ptr(D), O.shape[1], N.ptr(out))
+    return out

@@ -1,0 +1,121 @@
+"""Workload scenes for tests and bench, built with this package's sightpy API.
+
+These restate the scene *parameters* of the reference's example scripts (example1.py, example2.py,
+example3.py, example4.py, example_cornellbox.py) as functions of resolution and recursion depth, so
+the BASELINE.json configurations (e.g. example1 at 1920x1080 depth 5) can be built without editing
+the scripts.  `depth=None` keeps each primitive's own max_ray_depth from the script.
+tests/golden/gen_golden.py renders the reference's own scripts with the same overrides.
+"""
+import numpy as np
+
+from sightpy import (Scene, Sphere, Plane, Cuboid, Glossy, Refractive, ThinFilmInterference, Diffuse,
+                     Emissive, image, rgb, vec3)
+
+
+def _depth(scene, depth):
+    if depth is not None:
+        for p in scene.scene_primitives:
+            p.max_ray_depth = depth
+    return scene
+
+
+def example1(width=400, height=300, depth=None):
+    gold = Glossy(diff_color=rgb(1.0, 0.572, 0.184), n=vec3(0.15 + 3.58j, 0.4 + 2.37j, 1.54 + 1.91j),
+                  roughness=0.0, spec_coeff=0.2, diff_coeff=0.8)
+    blue = Glossy(diff_color=rgb(0.0, 0, 0.1), n=vec3(1.3 + 1.91j, 1.3 + 1.91j, 1.4 + 2.91j),
+                  roughness=0.2, spec_coeff=0.5, diff_coeff=0.3)
+    floor = Glossy(diff_color=image("checkered_floor.png", repeat=80.0), n=vec3(1.2 + 0.3j, 1.2 + 0.3j, 1.1 + 0.3j),
+                   roughness=0.2, spec_coeff=0.3, diff_coeff=0.9)
+    sc = Scene(ambient_color=rgb(0.05, 0.05, 0.05))
+    angle = -np.pi / 2 * 0.3
+    sc.add_Camera(look_from=vec3(2.5 * np.sin(angle), 0.25, 2.5 * np.cos(angle) - 1.5),
+                  look_at=vec3(0.0, 0.25, -3.0), screen_width=width, screen_height=height)
+    sc.add_DirectionalLight(Ldir=vec3(0.52, 0.45, -0.5), color=rgb(0.15, 0.15, 0.15))
+    sc.add(Sphere(material=gold, center=vec3(-0.75, 0.1, -3.0), radius=0.6, max_ray_depth=3))
+    sc.add(Sphere(material=blue, center=vec3(1.25, 0.1, -3.0), radius=0.6, max_ray_depth=3))
+    sc.add(Plane(material=floor, center=vec3(0, -0.5, -3.0), width=120.0, height=120.0,
+                 u_axis=vec3(1.0, 0, 0), v_axis=vec3(0, 0, -1.0), max_ray_depth=3))
+    sc.add_Background("stormydays.png")
+    return _depth(sc, depth)
+
+
+def example2(width=400, height=300, depth=None):
+    blue = Refractive(n=vec3(1.5 + 4e-8j, 1.5 + 4e-8j, 1.5 + 0.0j))
+    green = Refractive(n=vec3(1.5 + 4e-8j, 1.5 + 0.0j, 1.5 + 4e-8j))
+    red = Refractive(n=vec3(1.5 + 0.0j, 1.5 + 5e-8j, 1.5 + 5e-8j))
+    floor = Glossy(diff_color=image("checkered_floor.png", repeat=80.0), n=vec3(1.2 + 0.3j, 1.2 + 0.3j, 1.1 + 0.3j),
+                   roughness=0.2, spec_coeff=0.3, diff_coeff=0.9)
+    sc = Scene(ambient_color=rgb(0.05, 0.05, 0.05))
+    angle = np.pi / 2 * 0.3
+    sc.add_Camera(look_from=vec3(2.5 * np.sin(angle), 0.25, 2.5 * np.cos(angle) - 1.5),
+                  look_at=vec3(0.0, 0.25, -1.5), screen_width=width, screen_height=height)
+    sc.add_DirectionalLight(Ldir=vec3(0.52, 0.45, -0.5), color=rgb(0.15, 0.15, 0.15))
+    for mat, x in ((blue, -1.2), (green, 0.0), (red, 1.2)):
+        sc.add(Sphere(material=mat, center=vec3(x, 0.0, -1.5), radius=0.5, shadow=False, max_ray_depth=3))
+    sc.add(Plane(material=floor, center=vec3(0, -0.5, -3.0), width=120.0, height=120.0,
+                 u_axis=vec3(1.0, 0, 0), v_axis=vec3(0, 0, -1.0), max_ray_depth=3))
+    sc.add_Background("miramar.jpeg")
+    return _depth(sc, depth)
+
+
+def example3(width=400, height=300, depth=None):
+    floor = Glossy(diff_color=image("checkered_floor.png", repeat=2.0), roughness=0.2, spec_coeff=0.3,
+                   diff_coeff=0.7, n=vec3(2.2, 2.2, 2.2))
+    green = Refractive(n=vec3(1.5 + 4e-8j, 1.5 + 0.0j, 1.5 + 4e-8j))
+    sc = Scene()
+    sc.add_Camera(look_from=vec3(0.0, 0.25, 1.0), look_at=vec3(0.0, 0.25, -3.0), screen_width=width,
+                  screen_height=height)
+    sc.add_DirectionalLight(Ldir=vec3(0.0, 0.5, 0.5), color=rgb(0.5, 0.5, 0.5))
+    sc.add(Plane(material=floor, center=vec3(0, -0.5, -3.0), width=6.0, height=6.0, u_axis=vec3(1.0, 0, 0),
+                 v_axis=vec3(0, 0, -1.0), max_ray_depth=5))
+    cb = Cuboid(material=green, center=vec3(0.00, 0.0001, -0.8), width=0.9, height=1.0, length=0.4, shadow=False,
+                max_ray_depth=5)
+    cb.rotate(θ=30, u=vec3(0, 1, 0))
+    sc.add(cb)
+    sc.add_Background("stormydays.png")
+    return _depth(sc, depth)
+
+
+def example4(width=400, height=300, depth=None):
+    sc = Scene(ambient_color=rgb(0.01, 0.01, 0.01))
+    angle = -np.pi * 0.5
+    sc.add_Camera(screen_height=height, screen_width=width,
+                  look_from=vec3(4.0 * np.sin(angle), 0.00, 4.0 * np.cos(angle)), look_at=vec3(0.0, 0.05, 0.0))
+    bubble = ThinFilmInterference(thickness=330, noise=60.0)
+    sc.add(Sphere(material=bubble, center=vec3(1.0, 0.0, 1.5), radius=1.7, shadow=False, max_ray_depth=5))
+    sc.add_Background("lake.png", light_intensity=5.0, blur=10.0)
+    return _depth(sc, depth)
+
+
+def cornell(width=100, height=100, depth=None):
+    sc = Scene(ambient_color=rgb(0.00, 0.00, 0.00))
+    sc.add_Camera(screen_width=width, screen_height=height, look_from=vec3(278, 278, 800),
+                  look_at=vec3(278, 278, 0), focal_distance=1.0, field_of_view=40)
+    green = Diffuse(diff_color=rgb(0.12, 0.45, 0.15))
+    red = Diffuse(diff_color=rgb(0.65, 0.05, 0.05))
+    white = Diffuse(diff_color=rgb(0.73, 0.73, 0.73))
+    light = Emissive(color=rgb(15.0, 15.0, 15.0))
+    glass = Refractive(n=vec3(1.5 + 0.05e-8j, 1.5 + 0.02e-8j, 1.5 + 0.0j))
+    sc.add(Plane(material=light, center=vec3(213 + 130 / 2, 554, -227.0 - 105 / 2), width=130.0, height=105.0,
+                 u_axis=vec3(1.0, 0.0, 0), v_axis=vec3(0.0, 0, 1.0)), importance_sampled=True)
+    sc.add(Plane(material=white, center=vec3(555 / 2, 555 / 2, -555.0), width=555.0, height=555.0,
+                 u_axis=vec3(0.0, 1.0, 0), v_axis=vec3(1.0, 0, 0.0)))
+    sc.add(Plane(material=green, center=vec3(-0.0, 555 / 2, -555 / 2), width=555.0, height=555.0,
+                 u_axis=vec3(0.0, 1.0, 0), v_axis=vec3(0.0, 0, -1.0)))
+    sc.add(Plane(material=red, center=vec3(555.0, 555 / 2, -555 / 2), width=555.0, height=555.0,
+                 u_axis=vec3(0.0, 1.0, 0), v_axis=vec3(0.0, 0, -1.0)))
+    sc.add(Plane(material=white, center=vec3(555 / 2, 555, -555 / 2), width=555.0, height=555.0,
+                 u_axis=vec3(1.0, 0.0, 0), v_axis=vec3(0.0, 0, -1.0)))
+    sc.add(Plane(material=white, center=vec3(555 / 2, 0.0, -555 / 2), width=555.0, height=555.0,
+                 u_axis=vec3(1.0, 0.0, 0), v_axis=vec3(0.0, 0, -1.0)))
+    cb = Cuboid(material=white, center=vec3(182.5, 165, -285 - 160 / 2), width=165, height=165 * 2, length=165,
+                shadow=False)
+    cb.rotate(θ=15, u=vec3(0, 1, 0))
+    sc.add(cb)
+    sc.add(Sphere(material=glass, center=vec3(370.5, 165 / 2, -65 - 185 / 2), radius=165 / 2, shadow=False,
+                  max_ray_depth=3), importance_sampled=True)
+    return _depth(sc, depth)
+
+
+BUILDERS = {"example1": example1, "example2": example2, "example3": example3, "example4": example4,
+            "cornell": cornell}
