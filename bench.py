@@ -1,0 +1,238 @@
+"""Headline benchmark: Mrays/s (primary + secondary) on example1 at 1920x1080, depth 5, 6 spp
+(BASELINE.json configs[1]) through the C ABI of libsightpy_hip.so.
+
+One step = one full frame: every spp sample traced through every depth, plus the sRGB resolve, with
+the scene, camera tables and the sample jitter already resident in HBM (the jitter is the
+reference's numpy stream for seed 0, uploaded once before timing).  With N GPUs
+(torch.distributed, one process per GPU) the frame's rows are dealt round-robin in 8-row bands,
+each rank renders its shard and the uint8 tiles are gathered to rank 0 over RCCL; the frame is
+fixed, so scaling is strong.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config example1_1080p_d5]
+"""
+import argparse
+import ctypes
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+for p in (ROOT / "python-raytracer_amd", ROOT / "tests", ROOT / "oracle"):
+    sys.path.insert(0, str(p))
+
+BYTES_PER_RAY = 280  # algorithmic bytes per ray segment of the fp64 wavefront
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (builder, width, height, depth, spp, label)
+    "example1_1080p_d5": ("example1", 1920, 1080, 5, 6, "example1.py (spheres+plane) 1920x1080 depth 5, 6 spp"),
+    "example3_1080p_d8": ("example3", 1920, 1080, 8, 4, "example3.py (glass cuboid) 1920x1080 depth 8, 4 spp"),
+    "example4_4k_d6": ("example4", 3840, 2160, 6, 10, "example4.py (thin film) 3840x2160 depth 6, 10 spp"),
+    "cornell_800_s512": ("cornell", 800, 800, None, 512, "example_cornellbox.py 800x800, 512 spp (MC)"),
+    "example1_400x300_d3": ("example1", 400, 300, None, 6, "example1.py 400x300 depth 3, 6 spp"),
+}
+
+
+def shard_rows(height, world, rank, band=8):
+    rows = np.arange(height)
+    return rows[(rows // band) % world == rank]
+
+
+def cpu_baseline(builder, W, H, depth):
+    """Oracle (numpy port) on a bounded sample of the same workload: 1 spp over a row band."""
+    import sightpy_oracle as O
+    import scenes
+
+    sc = getattr(scenes, builder)(W, H, depth)
+    rows = max(8, min(H, int(H * 0.25)))
+    # band of `rows` rows through the middle of the image (floor, spheres and sky)
+    np.random.seed(1)
+    jit = sc.camera.draw_jitter(1)[0]
+    r0 = (H - rows) // 2
+    sel = slice(r0 * W, (r0 + rows) * W)
+    Oo, Do = O.primary_rays(sc.camera, jit)
+    Oo = np.broadcast_to(Oo, Do.shape)[:, sel]
+    Do = Do[:, sel]
+    counts = {}
+    t0 = time.perf_counter()
+    O.raycolor(sc, O.Rays(np.ascontiguousarray(Oo), np.ascontiguousarray(Do), O.scene_medium(sc), 0), counts)
+    dt = time.perf_counter() - t0
+    rays = sum(counts["depth"].values())
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": "oracle/sightpy_oracle.py (numpy restatement), 1 process, %d rows x %d px x 1 spp "
+                      "(%d rays, %.1f s) of the same scene" % (rows, W, rays, dt),
+            "cpu_model": platform.processor() or _cpu_model(), "host_cpus": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        for line in out.splitlines():
+            if "Model name" in line:
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
+    ap.add_argument("--rng", default="numpy", choices=["numpy", "device"],
+                    help="numpy: reference jitter stream resident in HBM; device: Philox raygen")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--spp", type=int, default=None)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("SIGHTPY_DEVICE", str(local))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    builder, W, H, depth, spp, label = CONFIGS[args.config]
+    if args.spp:
+        spp = args.spp
+    sc = getattr(scenes, builder)(W, H, depth)
+    lib, ctx = B.context()
+    B.upload(sc)
+    rows = shard_rows(H, world, rank) if world > 1 else np.arange(H)
+    npix = len(rows) * W
+    # resident inputs: jitter (reference stream, seed 0) in HBM
+    jit_dev = None
+    if args.rng == "numpy":
+        np.random.seed(0)
+        jit = np.random.rand(spp * 4 * H * W).reshape(spp, 4, H, W)[:, :, rows].reshape(spp, 4, npix)
+        jit = np.ascontiguousarray(jit)
+        p = ctypes.c_void_p()
+        N.check(lib, lib.srt_device_alloc(ctx, jit.nbytes, ctypes.byref(p)))
+        N.check(lib, lib.srt_memcpy(ctx, p, N.ptr(jit), jit.nbytes))
+        jit_dev = p
+        del jit
+    out_u8 = ctypes.c_void_p()
+    out_rgb = ctypes.c_void_p()
+    N.check(lib, lib.srt_device_alloc(ctx, 3 * npix, ctypes.byref(out_u8)))
+    N.check(lib, lib.srt_device_alloc(ctx, 3 * npix * 8, ctypes.byref(out_rgb)))
+    cd = B.camera_desc(sc.camera)
+    rows32 = np.ascontiguousarray(rows, dtype=np.int32)
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, len(rows), 0
+    a.rows = N.ptr(rows32)
+    a.jitter = jit_dev
+    a.seed = 12345
+    a.out_rgb, a.out_srgb8, a.out_hit_id = out_rgb, out_u8, None
+
+    gather = None
+    if dist is not None:
+        import torch
+
+        maxrows = max(len(shard_rows(H, world, r)) for r in range(world))
+        tile = torch.zeros(maxrows * W * 3, dtype=torch.uint8, device="cuda")
+        gather = (torch, tile, torch.empty(world * maxrows * W * 3, dtype=torch.uint8, device="cuda"))
+
+    def step(st):
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
+        if gather is not None:
+            torch, tile, full = gather
+            # rank tile -> torch buffer (device to device), then RCCL all-gather over xGMI
+            N.check(lib, lib.srt_memcpy(ctx, ctypes.c_void_p(tile.data_ptr()), out_u8, 3 * npix))
+            dist.all_gather_into_tensor(full, tile)
+
+    st = N.Stats()
+    for _ in range(args.warmup):
+        step(st)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+        N.check(lib, lib.srt_synchronize(ctx))
+
+    stats = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = N.Stats()
+        step(s)
+        stats.append(s.as_dict())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        rays_local = torch.tensor([stats[0]["total_rays"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(rays_local)
+        total_rays = float(rays_local.item())
+    else:
+        total_rays = float(stats[0]["total_rays"])
+
+    ms_step = elapsed / args.steps * 1e3
+    value = total_rays * args.steps / elapsed / 1e6
+    # roofline of the dominant kernel (depth-0 trace = raygen + trace; HIP events on its stream)
+    prim_ms = np.mean([s["ms_primary_kernel"] for s in stats])
+    trace_ms = np.mean([s["ms_trace_kernels"] for s in stats])
+    rpd = stats[0]["rays_per_depth"]
+    achieved = rpd[0] * BYTES_PER_RAY / (prim_ms * 1e-3) / 1e9
+    family = stats[0]["total_rays"] * BYTES_PER_RAY / (trace_ms * 1e-3) / 1e9
+    if rank == 0:
+        rec = {
+            "metric": "Mrays/sec (primary+secondary) at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
+            else "Mrays/sec (primary+secondary)",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: %s; jitter = reference numpy stream seed 0 (%s)" % (label, args.rng),
+            "config": {"workload": label, "width": W, "height": H, "max_ray_depth": depth, "spp": spp,
+                       "rays_per_frame": int(total_rays), "rays_per_depth_rank0": rpd,
+                       "shadow_rays_rank0": stats[0]["shadow_rays"], "parallelism": "row-band shards x%d" % world,
+                       "frame_ms": round(ms_step, 4)},
+            "roofline": {"bound": "hbm", "kernel": "k_trace<true> (depth-0 raygen+trace)",
+                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_ray": BYTES_PER_RAY, "kernel_ms": round(float(prim_ms), 4),
+                         "all_trace_kernels": {"ms": round(float(trace_ms), 4), "achieved_GBs": round(family, 2),
+                                               "frac": round(family / HBM_PEAK_GBS, 4)}},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth)
+        print(json.dumps(rec))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    lib.srt_device_free(ctx, out_u8)
+    lib.srt_device_free(ctx, out_rgb)
+    if jit_dev is not None:
+        lib.srt_device_free(ctx, jit_dev)
+
+
+if __name__ == "__main__":
+    main()

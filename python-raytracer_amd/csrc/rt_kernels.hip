@@ -334,11 +334,14 @@ int grid_for(int64_t n, int max_blocks) {
 
 // seed the queue from caller rays (get_raycolor): ray i -> shard i % NSHARD, slot i / NSHARD
 __global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, const double* O, const double* D,
-                                                     const int32_t* med, int64_t n, uint32_t depth, uint32_t dfl) {
+                                                     const int32_t* med, int64_t n, uint32_t depth, uint32_t dfl,
+                                                     uint32_t nmedia) {
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
         int64_t dst = (i % NSHARD) * seg + i / NSHARD;
+        uint32_t m = med ? (uint32_t)med[i] : 0u;
+        if (m >= nmedia) m = 0u;  // out-of-table medium index: scene.n
         queue_store(q, dst, d3{O[i], O[n + i], O[2 * n + i]}, d3{D[i], D[n + i], D[2 * n + i]}, d3{1.0, 1.0, 1.0},
-                    (uint32_t)i, pack_meta(med ? (uint32_t)med[i] : 0u, depth, dfl), mix32(0x7A11u, (uint32_t)i));
+                    (uint32_t)i, pack_meta(m, depth, dfl), mix32(0x7A11u, (uint32_t)i));
     }
 }
 
@@ -541,8 +544,21 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
         if (cc.type < 0 || cc.type > 3) return fail(SRT_ERR_ARG, "bad collider type");
         if (cc.material < 0 || cc.material >= d->n_materials) return fail(SRT_ERR_ARG, "collider material out of range");
     }
+    if (!d->media) return fail(SRT_ERR_ARG, "media table is null");
+    if (d->n_lights > 0 && d->n_colliders > 0 && !d->light_local) return fail(SRT_ERR_ARG, "light_local is null");
+    if (d->n_importance > 0 && !d->importance) return fail(SRT_ERR_ARG, "importance table is null");
+    if (d->n_textures > 0 && (!d->textures || (d->texel_bytes > 0 && !d->texels)))
+        return fail(SRT_ERR_ARG, "texture tables are null");
+    for (int i = 0; i < d->n_textures; ++i) {
+        const srt_texture& t = d->textures[i];
+        if (t.height <= 0 || t.width <= 0 || t.channels < 3 || t.channel0 < 0 || t.channel0 + 3 > t.channels ||
+            t.idx_h <= 0 || t.idx_w <= 0 || t.offset < 0 ||
+            t.offset + (int64_t)t.height * t.width * t.channels > d->texel_bytes)
+            return fail(SRT_ERR_ARG, "texture record out of the texel pool");
+    }
     for (int i = 0; i < d->n_materials; ++i) {
         const srt_material& m = d->materials[i];
+        if (m.type == SRT_GLOSSY && !d->glossy_f0) return fail(SRT_ERR_ARG, "glossy_f0 table is null");
         int texs[4] = {m.tex, m.tex_aux0, m.tex_aux1, m.normalmap};
         for (int t : texs)
             if (t >= d->n_textures) return fail(SRT_ERR_ARG, "material texture index out of range");
@@ -788,7 +804,7 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
         HIP_TRY(hipMemcpyAsync(c->counts + (int64_t)d0 * NSHARD, seed_counts, sizeof(seed_counts),
                                hipMemcpyHostToDevice, c->stream));
         hipLaunchKernelGGL(k_seed_queue, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->q[d0 & 1],
-                           c->seg, O, D, med, n, (uint32_t)d0, (uint32_t)a->diffuse_reflections);
+                           c->seg, O, D, med, n, (uint32_t)d0, (uint32_t)a->diffuse_reflections, (uint32_t)c->S.nmedia);
         HIP_TRY(hipGetLastError());
         TraceParams P = base_params(c, a->seed);
         P.fb = c->fb;

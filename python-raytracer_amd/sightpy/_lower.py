@@ -101,6 +101,8 @@ class _TexturePool:
             raise TypeError("textures must be uint8 images")
         if u8.ndim == 2:
             u8 = u8[:, :, None]
+        if u8.shape[2] < 3:  # grey images: replicate to RGB (device reads 3 channels per texel)
+            u8 = np.ascontiguousarray(np.repeat(u8[:, :, :1], 3, axis=2))
         key = id(u8) if u8.base is None else (id(u8.base), u8.__array_interface__["data"][0])
         if key not in self.offsets:
             self.offsets[key] = self.size

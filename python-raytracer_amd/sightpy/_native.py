@@ -152,8 +152,11 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         n = max(int(self.n_depths), 0)
+        rpd = [int(x) for x in self.rays_per_depth[:n]]
+        while rpd and rpd[-1] == 0:
+            rpd.pop()
         return {
-            "rays_per_depth": [int(x) for x in self.rays_per_depth[:n]],
+            "rays_per_depth": rpd,
             "total_rays": int(self.total_rays),
             "shadow_rays": int(self.shadow_rays),
             "passes": int(self.passes),

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Run a sequence of GPU steps on the gpurun box, each under its own time limit.
+# Usage: tools/gpu_session.sh STEP... where STEP is one of: smoke tests bench prof pmc bench_all
+# Stops at the first step that ends in a fault / abort / time limit (rc not in {0,1}).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONDONTWRITEBYTECODE=1
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "== $name: $*" >> gpurun_out/summary.txt
+  local t0=$(date +%s)
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a gpurun_out/summary.txt
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 900 python3 -m pytest tests/test_gpu.py -q -m gpu --timeout=300 -rf ;;
+    bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
+    bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    configs) for c in example3_1080p_d8 example4_4k_d6 cornell_800_s512; do run "bench_$c" 600 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline; done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
