@@ -10,11 +10,13 @@ fixed, so scaling is strong.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config example1_1080p_d5]
 """
+import os
+
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # the CPU baseline is a single-core number
 import argparse
 import ctypes
 import json
 import os
-import platform
 import subprocess
 import sys
 import time
@@ -44,30 +46,32 @@ def shard_rows(height, world, rank, band=8):
     return rows[(rows // band) % world == rank]
 
 
-def cpu_baseline(builder, W, H, depth):
-    """Oracle (numpy port) on a bounded sample of the same workload: 1 spp over a row band."""
+def cpu_baseline(builder, W, H, depth, spp, budget_s=20.0):
+    """Oracle (numpy port of the reference algorithm) timed on this host's CPU, one process, on the
+    same frame: samples are traced one after another until the frame is done or `budget_s` of CPU
+    time is spent (the sample count is reported)."""
     import sightpy_oracle as O
     import scenes
 
     sc = getattr(scenes, builder)(W, H, depth)
-    rows = max(8, min(H, int(H * 0.25)))
-    # band of `rows` rows through the middle of the image (floor, spheres and sky)
-    np.random.seed(1)
-    jit = sc.camera.draw_jitter(1)[0]
-    r0 = (H - rows) // 2
-    sel = slice(r0 * W, (r0 + rows) * W)
-    Oo, Do = O.primary_rays(sc.camera, jit)
-    Oo = np.broadcast_to(Oo, Do.shape)[:, sel]
-    Do = Do[:, sel]
+    np.random.seed(0)
+    jit = sc.camera.draw_jitter(spp)
     counts = {}
+    done = 0
     t0 = time.perf_counter()
-    O.raycolor(sc, O.Rays(np.ascontiguousarray(Oo), np.ascontiguousarray(Do), O.scene_medium(sc), 0), counts)
+    for s in range(spp):
+        Oo, Do = O.primary_rays(sc.camera, jit[s])
+        O.raycolor(sc, O.Rays(np.ascontiguousarray(np.broadcast_to(Oo, Do.shape)), Do, O.scene_medium(sc), 0), counts)
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
     dt = time.perf_counter() - t0
     rays = sum(counts["depth"].values())
-    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": "oracle/sightpy_oracle.py (numpy restatement), 1 process, %d rows x %d px x 1 spp "
-                      "(%d rays, %.1f s) of the same scene" % (rows, W, rays, dt),
-            "cpu_model": platform.processor() or _cpu_model(), "host_cpus": os.cpu_count()}
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": "oracle/sightpy_oracle.py (numpy restatement of the reference), 1 process, "
+                      "OPENBLAS_NUM_THREADS=1: %d of %d samples of the same %dx%d frame (%d rays, %.1f s)"
+                      % (done, spp, W, H, rays, dt),
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
 
 
 def _cpu_model():
@@ -91,6 +95,7 @@ def main():
                     help="numpy: reference jitter stream resident in HBM; device: Philox raygen")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--occupancy", type=int, default=0, help="experiment: kernel variant with this waves/SIMD bound")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,6 +118,8 @@ def main():
         spp = args.spp
     sc = getattr(scenes, builder)(W, H, depth)
     lib, ctx = B.context()
+    if args.occupancy:
+        N.check(lib, lib.srt_set_option(ctx, b"occupancy", args.occupancy))
     B.upload(sc)
     rows = shard_rows(H, world, rank) if world > 1 else np.arange(H)
     npix = len(rows) * W
@@ -223,7 +230,7 @@ def main():
                                                "frac": round(family / HBM_PEAK_GBS, 4)}},
         }
         if not args.no_cpu_baseline and world == 1:
-            rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth)
+            rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth, spp)
         print(json.dumps(rec))
     if dist is not None:
         dist.barrier()

@@ -16,6 +16,15 @@
 
 #include "../../include/sightpy_rt.h"
 
+// Scene tables are read-only while a kernel runs.  In the device compilation they are addressed
+// through the constant address space so that wave-uniform reads (the collider loop, the
+// per-material waterfall) become scalar loads into SGPRs instead of per-lane loads into VGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_RO __attribute__((address_space(4)))
+#else
+#define RT_RO
+#endif
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define RT_HD __host__ __device__ __forceinline__
@@ -44,7 +53,8 @@ struct d3 {
 };
 
 RT_HD d3 mk(double x, double y, double z) { return d3{x, y, z}; }
-RT_HD d3 ld3(const double* p) { return d3{p[0], p[1], p[2]}; }
+template <class P>
+RT_HD d3 ld3(P p) { return d3{p[0], p[1], p[2]}; }
 RT_HD d3 add(d3 a, d3 b) { return d3{a.x + b.x, a.y + b.y, a.z + b.z}; }
 RT_HD d3 sub(d3 a, d3 b) { return d3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RT_HD d3 mul(d3 a, d3 b) { return d3{a.x * b.x, a.y * b.y, a.z * b.z}; }
@@ -63,7 +73,8 @@ RT_HD d3 normalize(d3 v) {
 
 // vec3.matmul on arrays = np.tensordot(B, v) -> OpenBLAS dgemm: one fma chain per row
 // (vector3.py:93-97; order verified bit-exact against OpenBLAS 0.3.29)
-RT_HD d3 matmul_rows(const double* B, d3 v) {
+template <class P>
+RT_HD d3 matmul_rows(P B, d3 v) {
     return d3{fma(B[2], v.z, fma(B[1], v.y, B[0] * v.x)),
               fma(B[5], v.z, fma(B[4], v.y, B[3] * v.x)),
               fma(B[8], v.z, fma(B[7], v.y, B[6] * v.x))};
@@ -127,15 +138,15 @@ RT_HD cplx csqrt_np(cplx z) {
 
 // ---- scene view ---------------------------------------------------------------------------
 struct SceneView {
-    const srt_collider* col;
-    const srt_material* mat;
-    const srt_texture* tex;
-    const uint8_t* texels;
-    const srt_light* lights;
-    const double* media;
-    const double* glossy_f0;
-    const double* light_local;
-    const double* importance;
+    const RT_RO srt_collider* col;
+    const RT_RO srt_material* mat;
+    const RT_RO srt_texture* tex;
+    const RT_RO uint8_t* texels;
+    const RT_RO srt_light* lights;
+    const RT_RO double* media;
+    const RT_RO double* glossy_f0;
+    const RT_RO double* light_local;
+    const RT_RO double* importance;
     int ncol, nmat, ntex, nlights, nmedia, nimp;
     int nshadow;  // colliders flagged SRT_CF_SHADOW
     double ambient[3];
@@ -143,7 +154,7 @@ struct SceneView {
 
 // ---- ray/primitive intersection (returns distance; orientation through `o`) -----------------
 // sphere.py:26-52
-RT_HD double sphere_hit(const double* p, d3 O, d3 D, double& o) {
+RT_HD double sphere_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     d3 C = ld3(p);
     double b = 2.0 * dot(D, sub(O, C));
     double c = ((p[5] + dot(O, O)) - 2.0 * dot(C, O)) - p[6];
@@ -162,7 +173,7 @@ RT_HD double sphere_hit(const double* p, d3 O, d3 D, double& o) {
 }
 
 // plane.py:57-90 (rectangle: |u| <= w, |v| <= h in the plane basis)
-RT_HD double plane_hit(const double* p, d3 O, d3 D, double& o) {
+RT_HD double plane_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     d3 N = ld3(p + 3);
     double nd = dot(N, D);
     nd = (nd == 0.0) ? nd + 0.0001 : nd;
@@ -183,7 +194,7 @@ RT_HD double plane_hit(const double* p, d3 O, d3 D, double& o) {
 
 // cuboid.py:105-140 (slab test in the local basis).  `Dl` is D.matmul(basis); it is passed in
 // because for shadow rays D is a scalar vec3 whose matmul goes through BLAS gemv on the host.
-RT_HD double cuboid_hit_local(const double* p, d3 O, d3 Dl, double& o) {
+RT_HD double cuboid_hit_local(const RT_RO double* p, d3 O, d3 Dl, double& o) {
     d3 Ol = matmul_rows(p + 3, O);
     d3 f = d3{1.0 / Dl.x, 1.0 / Dl.y, 1.0 / Dl.z};
     double t1 = (p[12] - Ol.x) * f.x, t2 = (p[15] - Ol.x) * f.x;
@@ -196,12 +207,12 @@ RT_HD double cuboid_hit_local(const double* p, d3 O, d3 Dl, double& o) {
     o = 1.0;
     return tmin;
 }
-RT_HD double cuboid_hit(const double* p, d3 O, d3 D, double& o) {
+RT_HD double cuboid_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     return cuboid_hit_local(p, O, matmul_rows(p + 3, D), o);
 }
 
 // triangle.py:36-66 (plane through the centroid + edge half-spaces)
-RT_HD double triangle_hit(const double* p, d3 O, d3 D, double& o) {
+RT_HD double triangle_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     d3 N = ld3(p + 3);
     double nd = dot(N, D);
     nd = (nd == 0.0) ? nd + 0.0001 : nd;
@@ -220,7 +231,7 @@ RT_HD double triangle_hit(const double* p, d3 O, d3 D, double& o) {
     return FARAWAY;
 }
 
-RT_HD double collider_hit(const srt_collider& c, d3 O, d3 D, double& o) {
+RT_HD double collider_hit(const RT_RO srt_collider& c, d3 O, d3 D, double& o) {
     switch (c.type) {
         case SRT_SPHERE: return sphere_hit(c.p, O, D, o);
         case SRT_PLANE: return plane_hit(c.p, O, D, o);
@@ -231,7 +242,7 @@ RT_HD double collider_hit(const srt_collider& c, d3 O, d3 D, double& o) {
 
 // ---- normals and uv (per collider) ---------------------------------------------------------
 // cuboid.py:142-151: face normal picked by the largest scaled |local coordinate|
-RT_HD d3 cuboid_normal(const double* p, d3 P) {
+RT_HD d3 cuboid_normal(const RT_RO double* p, d3 P) {
     d3 L = matmul_rows(p + 3, sub(P, ld3(p)));
     double ax = p[39] * fabs(L.x), ay = p[40] * fabs(L.y), az = p[41] * fabs(L.z);
     double m = np_max(np_max(ax, ay), az);
@@ -240,7 +251,7 @@ RT_HD d3 cuboid_normal(const double* p, d3 P) {
 }
 
 // un-oriented collider normal at P (Collider.get_Normal)
-RT_HD d3 collider_normal(const srt_collider& c, d3 P) {
+RT_HD d3 collider_normal(const RT_RO srt_collider& c, d3 P) {
     switch (c.type) {
         case SRT_SPHERE: return mul(sub(P, ld3(c.p)), c.p[4]);  // sphere.py:54-56
         case SRT_PLANE: return ld3(c.p + 3);                       // plane.py:104-105
@@ -254,7 +265,7 @@ RT_HD double cross_coord(d3 ax, double sgn, d3 MC, double width, double shift) {
     d3 a = d3{ax.x * sgn, ax.y * sgn, ax.z * sgn};
     return ((((dot(a, MC) / width) * 2.0) * 0.985 + 1.0) / 2.0) + shift;
 }
-RT_HD void cuboid_uv(const double* p, d3 P, double& u, double& v) {
+RT_HD void cuboid_uv(const RT_RO double* p, d3 P, double& u, double& v) {
     d3 N = cuboid_normal(p, P);
     d3 MC = sub(P, ld3(p));
     d3 aw = ld3(p + 18), ah = ld3(p + 21), al = ld3(p + 24);
@@ -277,7 +288,7 @@ RT_HD void cuboid_uv(const double* p, d3 P, double& u, double& v) {
 }
 
 // Primitive.get_uv(hit) for the collider's primitive; returns false for the undefined Triangle uv
-RT_HD bool collider_uv(const srt_collider& c, d3 P, double& u, double& v) {
+RT_HD bool collider_uv(const RT_RO srt_collider& c, d3 P, double& u, double& v) {
     switch (c.type) {
         case SRT_SPHERE: {  // sphere.py:58-64
             d3 M = divs(sub(P, ld3(c.p)), c.p[3]);
@@ -311,33 +322,33 @@ RT_HD int64_t np_index(int64_t i, int64_t n, uint32_t& err) {
     }
     return i;
 }
-RT_HD const uint8_t* texel_at(const SceneView& S, const srt_texture& T, int64_t row, int64_t col, uint32_t& err) {
+RT_HD const RT_RO uint8_t* texel_at(const SceneView& S, const RT_RO srt_texture& T, int64_t row, int64_t col, uint32_t& err) {
     row = np_index(row, T.height, err);
     col = np_index(col, T.width, err);
     return S.texels + T.offset + (row * (int64_t)T.width + col) * T.channels + T.channel0;
 }
 // img[-(int(v*H*rep) % H), int(u*W*rep) % W] (texture.py:32-39, skybox.py:54-86)
-RT_HD const uint8_t* tex_uv(const SceneView& S, const srt_texture& T, double u, double v, uint32_t& err) {
+RT_HD const RT_RO uint8_t* tex_uv(const SceneView& S, const RT_RO srt_texture& T, double u, double v, uint32_t& err) {
     int64_t m = py_mod(np_trunc((v * (double)T.idx_h) * T.repeat), T.idx_h);
     int64_t col = py_mod(np_trunc((u * (double)T.idx_w) * T.repeat), T.idx_w);
     return texel_at(S, T, -m, col, err);
 }
 RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err) {
-    const srt_texture& T = S.tex[tid];
-    const uint8_t* px = tex_uv(S, T, u, v, err);
+    const RT_RO srt_texture& T = S.tex[tid];
+    const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
     return d3{T.lut[px[0]], T.lut[px[1]], T.lut[px[2]]};
 }
 
 // Material.get_Normal (material.py:18-36): collider normal (or normal map) times orientation
-RT_HD d3 shading_normal(const SceneView& S, const srt_collider& c, const srt_material& m, d3 P,
+RT_HD d3 shading_normal(const SceneView& S, const RT_RO srt_collider& c, const RT_RO srt_material& m, d3 P,
                         double orient, uint32_t& err) {
     if (m.normalmap >= 0) {
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
-        const srt_texture& T = S.tex[m.normalmap];
-        const uint8_t* px = tex_uv(S, T, u, v, err);
+        const RT_RO srt_texture& T = S.tex[m.normalmap];
+        const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
         d3 nm = d3{(T.lut[px[0]] - 0.5) * 2.0, (T.lut[px[1]] - 0.5) * 2.0, (T.lut[px[2]] - 0.5) * 2.0};
-        const double* ib = (c.type == SRT_PLANE) ? c.p + 16 : c.p + 30;
+        const RT_RO double* ib = (c.type == SRT_PLANE) ? c.p + 16 : c.p + 30;
         return mul(normalize(matmul_rows(ib, nm)), orient);
     }
     return mul(collider_normal(c, P), orient);
@@ -457,8 +468,15 @@ struct DiffuseGen {
     uint32_t medium, dfl;
 };
 
+// (1 - cos)^5 by repeated products; numpy evaluates `** 5` with its SIMD pow, both are within a
+// few ulp of the exact power (far inside the 1e-5 colour tolerance)
+RT_HD double pow5(double x) {
+    double x2 = x * x;
+    return (x2 * x2) * x;
+}
+
 RT_HD d3 schlick(d3 F0, double cos_t) {
-    double p = pow(1.0 - cos_t, 5.0);
+    double p = pow5(1.0 - cos_t);
     d3 one_m = rsub(1.0, F0);
     return add(F0, mul(one_m, p));
 }
@@ -480,7 +498,7 @@ RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L) {
     double best = FARAWAY;
     bool first = true;
     for (int c = 0; c < S.ncol; ++c) {
-        const srt_collider& cc = S.col[c];
+        const RT_RO srt_collider& cc = S.col[c];
         if (!(cc.flags & SRT_CF_SHADOW)) continue;
         double o, t;
         if (cc.type == SRT_CUBOID)
@@ -495,9 +513,9 @@ RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L) {
 
 // Glossy.get_color (glossy.py:25-110)
 template <class E>
-RT_HD void shade_glossy(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, double orient,
+RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, double orient,
                         E& em, uint32_t& err) {
-    const srt_material& m = S.mat[mi];
+    const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
     d3 N = shading_normal(S, c, m, P, orient, err);
     d3 diff;
@@ -513,7 +531,7 @@ RT_HD void shade_glossy(const SceneView& S, const srt_collider& c, int mi, const
     d3 nudged = add(P, mul(N, NUDGE));
     uint32_t med = meta_medium(r.meta);
     for (int l = 0; l < S.nlights; ++l) {
-        const srt_light& Lt = S.lights[l];
+        const RT_RO srt_light& Lt = S.lights[l];
         d3 L, lv;
         double dist;
         if (Lt.type == SRT_LIGHT_DIRECTIONAL) {
@@ -555,17 +573,17 @@ RT_HD void shade_glossy(const SceneView& S, const srt_collider& c, int mi, const
 
 // Refractive.get_color (refractive.py:24-123); `mc_u` is the uniform for the MC pick
 template <class E>
-RT_HD void shade_refractive(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t,
+RT_HD void shade_refractive(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t,
                             double orient, E& em, uint32_t& err, double mc_u) {
     if ((int)meta_depth(r.meta) >= c.max_ray_depth) return;  // black beyond max_ray_depth
-    const srt_material& m = S.mat[mi];
+    const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
     d3 N = shading_normal(S, c, m, P, orient, err);
     d3 V = mul(r.d, -1.0);
     uint32_t m1 = meta_medium(r.meta);
     uint32_t m2 = (orient == 1.0) ? (uint32_t)m.medium : 0u;
-    const double* n1 = S.media + m1 * 6;
-    const double* n2 = S.media + m2 * 6;
+    const RT_RO double* n1 = S.media + m1 * 6;
+    const RT_RO double* n2 = S.media + m2 * 6;
     double cos_i = dot(V, N);
     double s = 1.0 - cos_i * cos_i;
     double F[3], ratio[3];
@@ -615,28 +633,28 @@ RT_HD void shade_refractive(const SceneView& S, const srt_collider& c, int mi, c
 
 // ThinFilmInterference.get_color (thin_film_interference.py:24-115)
 template <class E>
-RT_HD void shade_thinfilm(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t,
+RT_HD void shade_thinfilm(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t,
                           double orient, E& em, uint32_t& err) {
     if ((int)meta_depth(r.meta) >= c.max_ray_depth) return;
-    const srt_material& m = S.mat[mi];
+    const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
     d3 N = shading_normal(S, c, m, P, orient, err);
     d3 V = mul(r.d, -1.0);
     double cos_i = dot(V, N);
-    const srt_texture& lut = S.tex[m.tex_aux0];
+    const RT_RO srt_texture& lut = S.tex[m.tex_aux0];
     int64_t li = np_trunc(cos_i * (double)lut.height);
     int64_t ti;
     if (m.flags & SRT_MF_NOISE) {
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
-        const srt_texture& nt = S.tex[m.tex_aux1];
+        const RT_RO srt_texture& nt = S.tex[m.tex_aux1];
         double nz = nt.lut[*tex_uv(S, nt, u, v, err)];
         double thick = m.p[0] + m.p[1] * (nz - 0.5);
         ti = np_trunc(thick);
     } else {
         ti = (int64_t)m.p[0];
     }
-    const uint8_t* px = texel_at(S, lut, li, ti, err);
+    const RT_RO uint8_t* px = texel_at(S, lut, li, ti, err);
     d3 F = d3{lut.lut[px[0]], lut.lut[px[1]], lut.lut[px[2]]};
     em.local(mul(ld3(S.ambient), F));
     uint32_t med = meta_medium(r.meta), dfl = meta_diffuse(r.meta);
@@ -646,16 +664,16 @@ RT_HD void shade_thinfilm(const SceneView& S, const srt_collider& c, int mi, con
 
 // SkyBox_Material.get_texture_color (skybox.py:51-94)
 template <class E>
-RT_HD void shade_sky(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, E& em,
+RT_HD void shade_sky(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, E& em,
                      uint32_t& err) {
-    const srt_material& m = S.mat[mi];
+    const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
     double u, v;
     if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
     d3 col = tex_rgb(S, m.tex, u, v, err);
     if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP)) {
-        const srt_texture& L = S.tex[m.tex_aux0];
-        const uint8_t* px = tex_uv(S, L, u, v, err);
+        const RT_RO srt_texture& L = S.tex[m.tex_aux0];
+        const RT_RO uint8_t* px = tex_uv(S, L, u, v, err);
         col = d3{col.x + m.p[0] * L.lut[px[0]], col.y + m.p[0] * L.lut[px[1]], col.z + m.p[0] * L.lut[px[2]]};
     }
     em.local(col);
@@ -663,9 +681,9 @@ RT_HD void shade_sky(const SceneView& S, const srt_collider& c, int mi, const Ra
 
 // Emissive.get_color (emissive.py:21-23)
 template <class E>
-RT_HD void shade_emissive(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, E& em,
+RT_HD void shade_emissive(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, E& em,
                           uint32_t& err) {
-    const srt_material& m = S.mat[mi];
+    const RT_RO srt_material& m = S.mat[mi];
     if (m.tex >= 0) {
         double u, v;
         d3 P = add(r.o, mul(r.d, t));
@@ -678,11 +696,11 @@ RT_HD void shade_emissive(const SceneView& S, const srt_collider& c, int mi, con
 
 // Diffuse.get_color (diffuse.py:25-124): no local colour; the children carry the estimate
 template <class E>
-RT_HD void shade_diffuse(const SceneView& S, const srt_collider& c, int mi, const Ray& r, double t, double orient,
+RT_HD void shade_diffuse(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, double orient,
                          E& em, uint32_t& err) {
     uint32_t dfl = meta_diffuse(r.meta);
     if (dfl >= 2) return;
-    const srt_material& m = S.mat[mi];
+    const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
     d3 N = shading_normal(S, c, m, P, orient, err);
     d3 diff;
@@ -713,7 +731,7 @@ RT_HD void onb(d3 w, d3& u, d3& v) {
 
 // One diffuse child: direction from the cosine PDF or the cosine/spherical-caps mixture
 // (utils/random.py:58-174), weight = w * clip(N.d) / pdf(d).
-RT_HD Child diffuse_child(const SceneView& S, const srt_material& m, const DiffuseGen& g, Rng& rng, uint32_t k) {
+RT_HD Child diffuse_child(const SceneView& S, const RT_RO srt_material& m, const DiffuseGen& g, Rng& rng, uint32_t k) {
     double pdf1w = m.p[3];
     double sel, dummy;
     rng.two(sel, dummy);
@@ -732,7 +750,7 @@ RT_HD Child diffuse_child(const SceneView& S, const srt_material& m, const Diffu
         rng.two(pick, a);
         int i = (int)(pick * (double)S.nimp);
         if (i >= S.nimp) i = S.nimp - 1;
-        const double* im = S.importance + 4 * i;
+        const RT_RO double* im = S.importance + 4 * i;
         d3 tc = sub(ld3(im), g.P);
         d3 w = normalize(tc);
         double dist = sqrt(dot(tc, tc));
@@ -751,7 +769,7 @@ RT_HD Child diffuse_child(const SceneView& S, const srt_material& m, const Diffu
     if (S.nimp > 0) {
         double caps_pdf = 0.0;
         for (int i = 0; i < S.nimp; ++i) {
-            const double* im = S.importance + 4 * i;
+            const RT_RO double* im = S.importance + 4 * i;
             d3 tc = sub(ld3(im), g.P);
             d3 w = normalize(tc);
             double dist = sqrt(dot(tc, tc));
@@ -766,18 +784,34 @@ RT_HD Child diffuse_child(const SceneView& S, const srt_material& m, const Diffu
     return mkchild(g.P, dir, mul(g.w, ndl / pdf), g.medium, g.dfl, 0x100u + k);
 }
 
+// Material-type bit masks: a kernel instantiated for MATS contains only those shading paths.
+constexpr uint32_t MAT_ALL = 0x3Fu;
+constexpr uint32_t mat_bit(int type) { return 1u << type; }
+
 // Shade one (ray, collider) hit with a per-lane (possibly divergent) material.
-template <class E>
+template <uint32_t MATS = MAT_ALL, class E>
 RT_HD void shade_hit(const SceneView& S, int cid, int mi, const Ray& r, double t, double orient, E& em,
                      uint32_t& err, double mc_u) {
-    const srt_collider& c = S.col[cid];
+    const RT_RO srt_collider& c = S.col[cid];
     switch (S.mat[mi].type) {
-        case SRT_GLOSSY: shade_glossy(S, c, mi, r, t, orient, em, err); break;
-        case SRT_REFRACTIVE: shade_refractive(S, c, mi, r, t, orient, em, err, mc_u); break;
-        case SRT_THINFILM: shade_thinfilm(S, c, mi, r, t, orient, em, err); break;
-        case SRT_DIFFUSE: shade_diffuse(S, c, mi, r, t, orient, em, err); break;
-        case SRT_EMISSIVE: shade_emissive(S, c, mi, r, t, em, err); break;
-        default: shade_sky(S, c, mi, r, t, em, err); break;
+        case SRT_GLOSSY:
+            if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy(S, c, mi, r, t, orient, em, err);
+            break;
+        case SRT_REFRACTIVE:
+            if (MATS & mat_bit(SRT_REFRACTIVE)) shade_refractive(S, c, mi, r, t, orient, em, err, mc_u);
+            break;
+        case SRT_THINFILM:
+            if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, mi, r, t, orient, em, err);
+            break;
+        case SRT_DIFFUSE:
+            if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse(S, c, mi, r, t, orient, em, err);
+            break;
+        case SRT_EMISSIVE:
+            if (MATS & mat_bit(SRT_EMISSIVE)) shade_emissive(S, c, mi, r, t, em, err);
+            break;
+        default:
+            if (MATS & mat_bit(SRT_SKY)) shade_sky(S, c, mi, r, t, em, err);
+            break;
     }
 }
 

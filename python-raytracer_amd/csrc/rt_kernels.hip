@@ -5,8 +5,9 @@
 // recursion is flattened into a breadth-first wavefront over structure-of-arrays ray queues in
 // HBM, one launch per depth:
 //
-//   k_trace<true>  depth 0: primary-ray generation (camera.py:51-85) fused with the trace step
-//   k_trace<false> depth d: read ray d from queue, nearest hit over all colliders, shade,
+//   k_primary      depth 0: primary-ray generation (camera.py:51-85) fused with the trace step,
+//                  one thread per pixel looping over the pass's samples
+//   k_trace        depth d: read ray d from queue, nearest hit over all colliders, shade,
 //                  add throughput * local colour to the framebuffer, append children to d+1
 //   k_resolve      spp average + sRGB + intensity clip + uint8 (scene.py:118-140)
 //
@@ -72,6 +73,7 @@ struct TraceParams {
     const int32_t* rows;
     const double* jitter;  // [spp][4][npix] (device) or null
     int sample_base;
+    int spp;           // samples of this pass (k_primary)
     int32_t* hit_out;  // [spp][npix] or null
 };
 
@@ -128,8 +130,15 @@ struct GpuEmit {
     uint32_t shard;
     uint32_t round;
     uint32_t* shadow_acc;
+    d3* acc;  // depth 0: the pixel's register accumulator (no framebuffer atomics)
 
-    __device__ void local(d3 c) const { fb_add(P.fb, P.npix, r.pix, r.w, c); }
+    __device__ void local(d3 c) const {
+        if (acc) {
+            if (!is_zero(c)) *acc = add(*acc, mul(r.w, c));
+        } else {
+            fb_add(P.fb, P.npix, r.pix, r.w, c);
+        }
+    }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void store(uint32_t slot, const Child& c, uint32_t path) const {
         if (slot < (uint64_t)P.seg) {
@@ -145,7 +154,7 @@ struct GpuEmit {
     }
     __device__ void diffuse(const DiffuseGen& g, int mi) const {
         uint32_t slot = wave_reserve(P.cnt_out + shard, (uint32_t)g.count);
-        const srt_material& m = P.S.mat[mi];
+        const auto& m = P.S.mat[mi];
         for (int k = 0; k < g.count; ++k) {
             Rng rng;
             const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
@@ -177,8 +186,10 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
 }
 
 // One trace step for one ray (all lanes of the wave call it; `active` masks the tail).
+// MATS: material types compiled into this instantiation (the host picks one covering the scene).
+template <uint32_t MATS>
 __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool active, uint32_t shard, uint32_t& err,
-                                          uint32_t& shadow, int32_t* hit_slot) {
+                                          uint32_t& shadow, int32_t* hit_slot, d3* acc) {
     const SceneView& S = P.S;
     double t = FARAWAY, o = FARAWAY;
     bool ties = false;
@@ -186,7 +197,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     if (active) id = nearest_hit(S, r.o, r.d, t, o, ties);
     if (hit_slot && active) *hit_slot = id;
     const int mat = (id >= 0) ? S.col[id].material : -1;
-    GpuEmit em{P, r, shard, 0u, &shadow};
+    GpuEmit em{P, r, shard, 0u, &shadow, acc};
     // waterfall over the materials present in the wave: material index and its parameters are
     // wave-uniform inside each pass (scalar loads, uniform type switch)
     uint64_t pending = __ballot(mat >= 0);
@@ -195,14 +206,27 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         const int m = __builtin_amdgcn_readfirstlane(__shfl(mat, lead));
         const bool mine = (mat == m);
         if (mine) {
-            const srt_collider& c = S.col[id];
+            const auto& c = S.col[id];
             switch (S.mat[m].type) {
-                case SRT_GLOSSY: shade_glossy(S, c, m, r, t, o, em, err); break;
-                case SRT_REFRACTIVE: shade_refractive(S, c, m, r, t, o, em, err, mc_uniform(P, r, id, 0)); break;
-                case SRT_THINFILM: shade_thinfilm(S, c, m, r, t, o, em, err); break;
-                case SRT_DIFFUSE: shade_diffuse(S, c, m, r, t, o, em, err); break;
-                case SRT_EMISSIVE: shade_emissive(S, c, m, r, t, em, err); break;
-                default: shade_sky(S, c, m, r, t, em, err); break;
+                case SRT_GLOSSY:
+                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy(S, c, m, r, t, o, em, err);
+                    break;
+                case SRT_REFRACTIVE:
+                    if (MATS & mat_bit(SRT_REFRACTIVE))
+                        shade_refractive(S, c, m, r, t, o, em, err, mc_uniform(P, r, id, 0));
+                    break;
+                case SRT_THINFILM:
+                    if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, m, r, t, o, em, err);
+                    break;
+                case SRT_DIFFUSE:
+                    if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse(S, c, m, r, t, o, em, err);
+                    break;
+                case SRT_EMISSIVE:
+                    if (MATS & mat_bit(SRT_EMISSIVE)) shade_emissive(S, c, m, r, t, em, err);
+                    break;
+                default:
+                    if (MATS & mat_bit(SRT_SKY)) shade_sky(S, c, m, r, t, em, err);
+                    break;
             }
         }
         pending &= ~__ballot(mine);
@@ -213,63 +237,113 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         for (int c = id + 1; c < S.ncol; ++c) {
             double oc;
             if (collider_hit(S.col[c], r.o, r.d, oc) == t) {
-                GpuEmit et{P, r, shard, round++, &shadow};
-                shade_hit(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(P, r, c, round - 1));
+                GpuEmit et{P, r, shard, round++, &shadow, acc};
+                shade_hit<MATS>(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(P, r, c, round - 1));
             }
         }
     }
 }
 
-template <bool PRIMARY>
-__global__ __launch_bounds__(BLOCK) void k_trace(TraceParams P) {
+// Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
+// (camera.py:51-85) and tracing it; the pixel's depth-0 colour is summed in registers and added to
+// the framebuffer once (no other thread touches the pixel during this launch).
+template <uint32_t MATS, int OCC = 1>
+__global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
+    const TraceParams& P = P0;
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
     uint32_t shadow = 0;
-    if (PRIMARY) {
-        const int64_t n = P.n_primary;
-        for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
-            const int64_t i = base + threadIdx.x;
-            const bool active = i < n;
+    const int64_t n = P.npix;
+    for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const bool active = i < n;
+        const uint32_t p = active ? (uint32_t)i : 0u;
+        const uint32_t lr = p / (uint32_t)P.cam.width;
+        const uint32_t col = p - lr * (uint32_t)P.cam.width;
+        const int grow = active ? P.rows[lr] : 0;
+        const double xc = active ? P.cam.xs[col] : 0.0, yr = active ? P.cam.ys[grow] : 0.0;
+        d3 acc = d3{0.0, 0.0, 0.0};
+        for (int s = 0; s < P.spp; ++s) {
             Ray r;
             r.o = r.d = d3{0.0, 0.0, 0.0};
             r.w = d3{1.0, 1.0, 1.0};
             r.meta = pack_meta(0, 0, 0);
-            r.pix = 0; r.path = 0;
-            int s_local = 0;
+            r.pix = p;
+            r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
             if (active) {
-                s_local = (int)(i / P.npix);
-                uint32_t p = (uint32_t)(i - (int64_t)s_local * P.npix);
-                uint32_t lr = p / (uint32_t)P.cam.width;
-                uint32_t col = p - lr * (uint32_t)P.cam.width;
-                int grow = P.rows[lr];
                 double j[4];
-                primary_uniforms(P, s_local, p, (uint32_t)grow * (uint32_t)P.cam.width + col, j);
-                primary_ray(P.cam, P.cam.xs[col], P.cam.ys[grow], j, r.o, r.d);
-                r.pix = p;
-                r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s_local));
+                primary_uniforms(P, s, p, (uint32_t)grow * (uint32_t)P.cam.width + col, j);
+                primary_ray(P.cam, xc, yr, j, r.o, r.d);
             }
-            int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s_local * P.npix + r.pix : nullptr;
-            trace_one(P, r, active, shard, err, shadow, hs);
+            int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
+            trace_one<MATS>(P, r, active, shard, err, shadow, hs, &acc);
         }
-    } else {
-        const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
-        const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
-        const int64_t off = (int64_t)shard * P.seg;
-        for (int64_t base = blk * BLOCK; base < n; base += nblk * BLOCK) {
-            const int64_t i = base + threadIdx.x;
-            const bool active = i < n;
-            Ray r;
-            if (active) {
-                r = queue_load(P.qin, off + i);
-            } else {
-                r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
-                r.pix = 0; r.meta = 0; r.path = 0;
-            }
-            trace_one(P, r, active, shard, err, shadow, nullptr);
+        if (active && !is_zero(acc)) {
+            P.fb[p] += acc.x;
+            P.fb[P.npix + p] += acc.y;
+            P.fb[2 * P.npix + p] += acc.z;
         }
     }
     if (err) atomicOr(&P.flags[0], err);
     if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+}
+
+// Depth d >= 1: blocks b, b + NSHARD, ... drain input shard b % NSHARD and append to output shard
+// b % NSHARD.
+template <uint32_t MATS, int OCC = 1>
+__global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
+    const TraceParams& P = P0;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    uint32_t err = 0;
+    uint32_t shadow = 0;
+    const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
+    const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
+    const int64_t off = (int64_t)shard * P.seg;
+    for (int64_t base = blk * BLOCK; base < n; base += nblk * BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const bool active = i < n;
+        Ray r;
+        if (active) {
+            r = queue_load(P.qin, off + i);
+        } else {
+            r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
+            r.pix = 0; r.meta = 0; r.path = 0;
+        }
+        trace_one<MATS>(P, r, active, shard, err, shadow, nullptr, nullptr);
+    }
+    if (err) atomicOr(&P.flags[0], err);
+    if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+}
+
+// Kernel variants by the material types they contain; the host picks the first covering the scene.
+constexpr uint32_t MATS_GLOSSY_SKY = mat_bit(SRT_GLOSSY) | mat_bit(SRT_SKY);
+constexpr uint32_t MATS_DIELECTRIC = MATS_GLOSSY_SKY | mat_bit(SRT_REFRACTIVE) | mat_bit(SRT_EMISSIVE);
+constexpr uint32_t MATS_FILM = mat_bit(SRT_THINFILM) | mat_bit(SRT_SKY) | mat_bit(SRT_GLOSSY);
+constexpr uint32_t MATS_MC = mat_bit(SRT_DIFFUSE) | mat_bit(SRT_EMISSIVE) | mat_bit(SRT_REFRACTIVE);
+struct Variant {
+    uint32_t mats;
+    void (*primary)(TraceParams);
+    void (*trace)(TraceParams);
+};
+// occupancy experiments for the headline scene (srt_set_option "occupancy" = 2, 3, 4)
+const Variant OCC_VARIANTS[] = {
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 2>, k_trace<MATS_GLOSSY_SKY, 2>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>},
+};
+int g_occupancy = 0;
+const Variant VARIANTS[] = {
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>},
+    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC>},
+    {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>},
+    {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>},
+    {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>},
+};
+const Variant& pick_variant(uint32_t mats) {
+    if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
+    for (const Variant& v : VARIANTS)
+        if ((v.mats & mats) == mats) return v;
+    return VARIANTS[sizeof(VARIANTS) / sizeof(VARIANTS[0]) - 1];
 }
 
 __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npix, double inv_spp_div, double spp,
@@ -298,12 +372,12 @@ __global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O,
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_intersect_one(srt_collider c, const double* O, const double* D, int64_t n,
-                                                        double* out) {
+__global__ __launch_bounds__(BLOCK) void k_intersect_one(const RT_RO srt_collider* c, const double* O,
+                                                        const double* D, int64_t n, double* out) {
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
         d3 o = d3{O[i], O[n + i], O[2 * n + i]}, d = d3{D[i], D[n + i], D[2 * n + i]};
         double orient;
-        double t = collider_hit(c, o, d, orient);
+        double t = collider_hit(*c, o, d, orient);
         out[i] = t;
         out[n + i] = orient;
     }
@@ -358,6 +432,7 @@ struct srt_ctx {
     int max_depth = 0;
     int has_diffuse = 0;
     int fanout = 1;
+    uint32_t mats = 0;  // material types present (selects the kernel variant)
     std::vector<void*> scene_bufs;
     // ray queues: 2 x NSHARD segments of `seg` rays
     Queue q[2]{};
@@ -531,6 +606,7 @@ int srt_destroy(srt_ctx* c) {
 int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
     if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
+    if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
     return fail(SRT_ERR_ARG, std::string("unknown option ") + key);
 }
@@ -589,8 +665,11 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     if ((rc = upload(c, d->glossy_f0, (int64_t)d->n_materials * d->n_media * 3, &f0))) return rc;
     if ((rc = upload(c, d->light_local, (int64_t)d->n_lights * d->n_colliders * 3, &ll))) return rc;
     if ((rc = upload(c, d->importance, (int64_t)d->n_importance * 4, &imp))) return rc;
-    S.col = col; S.mat = mat; S.tex = tex; S.texels = texels; S.lights = lights;
-    S.media = media; S.glossy_f0 = f0; S.light_local = ll; S.importance = imp;
+    // (casts: in the device compilation the SceneView fields are constant-address-space pointers)
+    S.col = (decltype(S.col))col; S.mat = (decltype(S.mat))mat; S.tex = (decltype(S.tex))tex;
+    S.texels = (decltype(S.texels))texels; S.lights = (decltype(S.lights))lights;
+    S.media = (decltype(S.media))media; S.glossy_f0 = (decltype(S.glossy_f0))f0;
+    S.light_local = (decltype(S.light_local))ll; S.importance = (decltype(S.importance))imp;
     S.ncol = d->n_colliders; S.nmat = d->n_materials; S.ntex = d->n_textures; S.nlights = d->n_lights;
     S.nmedia = d->n_media; S.nimp = d->n_importance;
     S.nshadow = 0;
@@ -607,6 +686,8 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     c->S = S;
     c->max_depth = std::max(0, (int)d->max_ray_depth);
     c->fanout = fan;
+    c->mats = 0;
+    for (int i = 0; i < d->n_materials; ++i) c->mats |= mat_bit(d->materials[i].type);
     c->has_scene = true;
     return SRT_OK;
 }
@@ -678,6 +759,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         P.cam.ys = c->ys;
         P.rows = c->rows;
         P.sample_base = a->sample_base + s0;
+        P.spp = ns;
         if (a->jitter) {
             const double* src = a->jitter + (int64_t)s0 * 4 * npix;
             if (jit_dev) {
@@ -694,7 +776,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         P.qout = c->q[1];
         P.cnt_out = c->counts + NSHARD;
         HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-        hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(nrays, c->max_blocks)), dim3(BLOCK), 0, c->stream, P);
+        const Variant& V = pick_variant(c->mats);
+        hipLaunchKernelGGL(V.primary, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, P);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev[1], c->stream));
         for (int d = 1; d <= dcap; ++d) {
@@ -703,7 +786,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.qout = c->q[(d + 1) & 1];
             P.cnt_in = c->counts + (int64_t)d * NSHARD;
             P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(k_trace<false>, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
+            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(c->ev[1 + d], c->stream));
         }
@@ -809,13 +892,14 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
         TraceParams P = base_params(c, a->seed);
         P.fb = c->fb;
         P.npix = n;
+        const Variant& V = pick_variant(c->mats);
         for (int d = d0; d <= dlast; ++d) {
             P.depth = d;
             P.qin = c->q[d & 1];
             P.qout = c->q[(d + 1) & 1];
             P.cnt_in = c->counts + (int64_t)d * NSHARD;
             P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(k_trace<false>, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
+            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
             HIP_TRY(hipGetLastError());
         }
         uint32_t flags[2];
@@ -883,16 +967,20 @@ int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O,
     if (n <= 0) return SRT_OK;
     HIP_TRY(hipSetDevice(c->device));
     double *dO, *dD, *dout;
+    srt_collider* dcol;
     HIP_TRY(dalloc(&dO, 3 * n));
     HIP_TRY(dalloc(&dD, 3 * n));
     HIP_TRY(dalloc(&dout, 2 * n));
+    HIP_TRY(dalloc(&dcol, 1));
     HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
-    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, *col, dO, dD, n,
+    HIP_TRY(hipMemcpy(dcol, col, sizeof(srt_collider), hipMemcpyDefault));
+    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, (const RT_RO srt_collider*)dcol, dO, dD, n,
                        dout);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(out, dout, (size_t)2 * n * 8, hipMemcpyDefault));
+    (void)hipFree(dcol);
     (void)hipFree(dO);
     (void)hipFree(dD);
     (void)hipFree(dout);

@@ -69,6 +69,13 @@ def _planar(v, n=None):
     return np.ascontiguousarray(np.stack([np.broadcast_to(c.reshape(-1) if c.ndim else c, (n,)) for c in comps]))
 
 
+def _default_seed():
+    """Seed for the device RNG derived from numpy's global RNG state WITHOUT consuming it (the
+    reference's render consumes only the camera draws from the parent's stream)."""
+    key, pos = np.random.get_state()[1:3]
+    return (int(key[pos % 624]) << 32 | int(key[(pos + 397) % 624])) ^ (int(pos) * 0x9E3779B97F4A7C15) & (2**64 - 1)
+
+
 def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False):
     """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG."""
     lib, ctx = context()
@@ -91,7 +98,7 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
         if j.shape != (spp, 4, npix):
             raise ValueError("jitter must have shape (spp, 4, %d)" % npix)
         a.jitter = N.ptr(j)
-    a.seed = int(seed if seed is not None else np.random.randint(0, 2**63 - 1, dtype=np.int64)) & (2**64 - 1)
+    a.seed = int(seed if seed is not None else _default_seed()) & (2**64 - 1)
     rgb = np.empty((3, npix)) if want_rgb else None
     u8 = np.empty((npix, 3), dtype=np.uint8)
     hits = np.empty((spp, npix), dtype=np.int32) if want_hits else None
@@ -128,7 +135,7 @@ def trace_rays(ray, scene, seed=None, return_stats=False):
     a.origin, a.dir, a.medium = N.ptr(O), N.ptr(D), N.ptr(med)
     a.depth = int(ray.depth)
     a.diffuse_reflections = int(ray.diffuse_reflections)
-    a.seed = int(seed if seed is not None else np.random.randint(0, 2**63 - 1, dtype=np.int64))
+    a.seed = int(seed if seed is not None else _default_seed()) & (2**64 - 1)
     a.out_rgb = N.ptr(out)
     st = N.Stats()
     N.check(lib, lib.srt_trace(ctx, ctypes.byref(a), ctypes.byref(st)))
