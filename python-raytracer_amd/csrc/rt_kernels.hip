@@ -372,8 +372,11 @@ __global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O,
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_intersect_one(const RT_RO srt_collider* c, const double* O,
+__global__ __launch_bounds__(BLOCK) void k_intersect_one(const srt_collider* c_generic, const double* O,
                                                         const double* D, int64_t n, double* out) {
+    // generic pointer in the signature (kernel arguments stay in the global address space),
+    // read through the constant address space inside
+    const RT_RO srt_collider* c = (const RT_RO srt_collider*)c_generic;
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
         d3 o = d3{O[i], O[n + i], O[2 * n + i]}, d = d3{D[i], D[n + i], D[2 * n + i]};
         double orient;
@@ -975,7 +978,7 @@ int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O,
     HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dcol, col, sizeof(srt_collider), hipMemcpyDefault));
-    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, (const RT_RO srt_collider*)dcol, dO, dD, n,
+    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, dcol, dO, dD, n,
                        dout);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));

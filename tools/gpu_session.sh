@@ -25,6 +25,7 @@ for step in "$@"; do
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     configs) for c in example3_1080p_d8 example4_4k_d6 cornell_800_s512; do run "bench_$c" 600 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline; done ;;
+    occ) for o in 0 2 3 4; do run "bench_occ$o" 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --occupancy $o; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
