@@ -78,7 +78,8 @@ enum {
  *            16-24 inverse_basis_matrix (row-major)
  *   CUBOID   0-2 center, 3-11 basis_matrix (row-major), 12-14 lb_local_basis,
  *            15-17 rt_local_basis, 18-20 ax_w, 21-23 ax_h, 24-26 ax_l, 27 width, 28 height,
- *            29 length, 30-38 inverse_basis_matrix (row-major), 39-41 (1/width,1/height,1/length)
+ *            29 length, 30-38 inverse_basis_matrix (row-major), 39-41 (1/width,1/height,1/length),
+ *            42 1.0 if basis_matrix is exactly the identity (else 0.0)
  *   TRIANGLE 0-2 centroid, 3-5 normal, 6-8 p1, 9-11 p2, 12-14 p3, 15-17 n31, 18-20 n12,
  *            21-23 n23
  */

@@ -88,11 +88,16 @@ RT_HD double np_clip(double x, double lo, double hi) { return np_min(np_max(x, l
 RT_HD double np_sign(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x)); }
 
 // ndarray.astype(int) of float64: truncation; out-of-range / NaN give INT64_MIN (x86 cvttsd2si)
+// (fast path: one v_cvt_i32_f64 when the value fits 32 bits, which texel indices always do)
 RT_HD int64_t np_trunc(double x) {
+    if (x > -2147483648.0 && x < 2147483648.0) return (int64_t)(int32_t)x;
     return (x > -9.2e18 && x < 9.2e18) ? (int64_t)x : (int64_t)(-9223372036854775807LL - 1);
 }
-// Python/numpy integer floor-mod (result has the sign of m)
+// Python/numpy integer floor-mod (result has the sign of m); 64-bit division is emulated on the
+// GPU, so in-range and 32-bit operands take cheaper paths with identical results
 RT_HD int64_t py_mod(int64_t a, int64_t m) {
+    if (a >= 0 && a < m) return a;
+    if (a >= 0 && a <= 0x7FFFFFFFLL && m > 0 && m <= 0x7FFFFFFFLL) return (int64_t)((uint32_t)a % (uint32_t)m);
     int64_t r = a % m;
     return (r != 0 && (r < 0) != (m < 0)) ? r + m : r;
 }
@@ -194,8 +199,12 @@ RT_HD double plane_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
 
 // cuboid.py:105-140 (slab test in the local basis).  `Dl` is D.matmul(basis); it is passed in
 // because for shadow rays D is a scalar vec3 whose matmul goes through BLAS gemv on the host.
+// p[42] != 0: the basis is exactly the identity (every SkyBox, unrotated cuboids).  The fma chain
+// then returns its input except for the sign of a zero component, which changes no result here
+// (|.| and np.sign ignore it; an axis-parallel slab gives t = +-inf pairs that either miss on
+// both signs or span (-inf, inf) and drop out of the min/max), so the matmuls are skipped.
 RT_HD double cuboid_hit_local(const RT_RO double* p, d3 O, d3 Dl, double& o) {
-    d3 Ol = matmul_rows(p + 3, O);
+    d3 Ol = (p[42] != 0.0) ? O : matmul_rows(p + 3, O);
     d3 f = d3{1.0 / Dl.x, 1.0 / Dl.y, 1.0 / Dl.z};
     double t1 = (p[12] - Ol.x) * f.x, t2 = (p[15] - Ol.x) * f.x;
     double t3 = (p[13] - Ol.y) * f.y, t4 = (p[16] - Ol.y) * f.y;
@@ -208,7 +217,7 @@ RT_HD double cuboid_hit_local(const RT_RO double* p, d3 O, d3 Dl, double& o) {
     return tmin;
 }
 RT_HD double cuboid_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
-    return cuboid_hit_local(p, O, matmul_rows(p + 3, D), o);
+    return cuboid_hit_local(p, O, (p[42] != 0.0) ? D : matmul_rows(p + 3, D), o);
 }
 
 // triangle.py:36-66 (plane through the centroid + edge half-spaces)
@@ -243,11 +252,12 @@ RT_HD double collider_hit(const RT_RO srt_collider& c, d3 O, d3 D, double& o) {
 // ---- normals and uv (per collider) ---------------------------------------------------------
 // cuboid.py:142-151: face normal picked by the largest scaled |local coordinate|
 RT_HD d3 cuboid_normal(const RT_RO double* p, d3 P) {
-    d3 L = matmul_rows(p + 3, sub(P, ld3(p)));
+    const bool axis = p[42] != 0.0;
+    d3 L = axis ? sub(P, ld3(p)) : matmul_rows(p + 3, sub(P, ld3(p)));
     double ax = p[39] * fabs(L.x), ay = p[40] * fabs(L.y), az = p[41] * fabs(L.z);
     double m = np_max(np_max(ax, ay), az);
     d3 s = d3{m == ax ? np_sign(L.x) : 0.0, m == ay ? np_sign(L.y) : 0.0, m == az ? np_sign(L.z) : 0.0};
-    return matmul_rows(p + 30, s);
+    return axis ? s : matmul_rows(p + 30, s);
 }
 
 // un-oriented collider normal at P (Collider.get_Normal)
@@ -335,6 +345,9 @@ RT_HD const RT_RO uint8_t* tex_uv(const SceneView& S, const RT_RO srt_texture& T
 }
 RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err) {
     const RT_RO srt_texture& T = S.tex[tid];
+#ifdef RT_ABL_TEX  // diagnostic build only: no gathers
+    return d3{u * T.repeat, v, u + v};
+#endif
     const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
     return d3{T.lut[px[0]], T.lut[px[1]], T.lut[px[2]]};
 }
@@ -547,7 +560,11 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
         if (Lt.type != SRT_LIGHT_DIRECTIONAL) lv = mul(divs(lv, dist * dist), 100.0);
         d3 H = normalize(add(L, V));
         double seelight = 1.0;
+#ifdef RT_ABL_SHADOW  // diagnostic build only: time without the shadow test
+        if (false) {
+#else
         if (S.nshadow > 0) {
+#endif
             double ln = shadow_nearest(S, l, nudged, L);
             seelight = (ln >= dist) ? 1.0 : 0.0;
             em.shadow(1);
@@ -557,7 +574,11 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
             d3 F0 = ld3(S.glossy_f0 + ((int64_t)mi * S.nmedia + med) * 3);
             double cos_t = np_clip(dot(V, H), 0.0, 1.0);
             d3 F = schlick(F0, cos_t);
+#ifdef RT_ABL_POW  // diagnostic build only
+            double Dphong = (pow5(np_clip(dot(N, H), 0.0, 1.0)) * m.p[5]) / m.p[6];
+#else
             double Dphong = (pow(np_clip(dot(N, H), 0.0, 1.0), m.p[4]) * m.p[5]) / m.p[6];
+#endif
             double den = 4.0 * np_clip(dot(N, V) * NdotL, 0.001, 1.0);
             d3 spec = mul(mul(mul(divs(mul(F, Dphong), den), seelight), lv), m.p[7]);
             color = add(color, spec);

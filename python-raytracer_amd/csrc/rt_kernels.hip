@@ -96,6 +96,10 @@ __device__ __forceinline__ Ray queue_load(const Queue& q, int64_t i) {
 
 __device__ __forceinline__ void fb_add(double* fb, int64_t npix, uint32_t pix, d3 w, d3 c) {
     if (is_zero(c)) return;  // adding an exact zero is a no-op (framebuffer starts at +0.0)
+#ifdef RT_ABL_FB  // diagnostic build only: no framebuffer atomics
+    if (w.x * c.x == 12345.678) fb[pix] = 0.0;
+    return;
+#endif
     unsafeAtomicAdd(fb + pix, w.x * c.x);
     unsafeAtomicAdd(fb + npix + pix, w.y * c.y);
     unsafeAtomicAdd(fb + 2 * npix + pix, w.z * c.z);
@@ -118,6 +122,10 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t cnt) {
         below += lanes_below(m) << b;
     }
     uint32_t base = 0;
+#ifdef RT_ABL_APPEND  // diagnostic build only: counts kept, slots not waited for (wrong images)
+    if (lanes_below(__ballot(1)) == 0) atomicAdd(ctr, total);
+    return ((blockIdx.x * 256u + threadIdx.x) * 2u + below % 2u) % 400000u;
+#endif
     if (lanes_below(__ballot(1)) == 0) base = atomicAdd(ctr, total);  // first active lane
     base = __builtin_amdgcn_readfirstlane(base);
     return base + below;
@@ -141,6 +149,10 @@ struct GpuEmit {
     }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void store(uint32_t slot, const Child& c, uint32_t path) const {
+#ifdef RT_ABL_QSTORE  // diagnostic build only: no queue stores
+        if (c.o.x == 12345.678) P.flags[1] = path;
+        return;
+#endif
         if (slot < (uint64_t)P.seg) {
             queue_store(P.qout, (int64_t)shard * P.seg + slot, c.o, c.d, mul(r.w, c.w), r.pix,
                         pack_meta(c.medium, meta_depth(r.meta) + 1, c.dfl), path);
@@ -247,7 +259,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
 // Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
 // (camera.py:51-85) and tracing it; the pixel's depth-0 colour is summed in registers and added to
 // the framebuffer once (no other thread touches the pixel during this launch).
-template <uint32_t MATS, int OCC = 1>
+template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     const TraceParams& P = P0;
     const uint32_t shard = blockIdx.x % NSHARD;
@@ -290,7 +302,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
 
 // Depth d >= 1: blocks b, b + NSHARD, ... drain input shard b % NSHARD and append to output shard
 // b % NSHARD.
-template <uint32_t MATS, int OCC = 1>
+template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
     const TraceParams& P = P0;
     const uint32_t shard = blockIdx.x % NSHARD;
@@ -325,9 +337,10 @@ struct Variant {
     void (*primary)(TraceParams);
     void (*trace)(TraceParams);
 };
-// occupancy experiments for the headline scene (srt_set_option "occupancy" = 2, 3, 4)
+// occupancy experiments for the headline scene (srt_set_option "occupancy" = 1 (index 2), 3, 4);
+// the default instantiations use 2 waves/SIMD, the fastest measured (profiles/)
 const Variant OCC_VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 2>, k_trace<MATS_GLOSSY_SKY, 2>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>},
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>},
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>},
 };

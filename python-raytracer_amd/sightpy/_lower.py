@@ -167,6 +167,8 @@ def collider_record(c):
         p[27], p[28], p[29] = c.width, c.height, c.length
         p[30:39] = np.asarray(c.inverse_basis_matrix, dtype=np.float64).reshape(-1)
         p[39], p[40], p[41] = 1.0 / c.width, 1.0 / c.height, 1.0 / c.length
+        eye = np.eye(3)
+        p[42] = 1.0 if (np.array_equal(c.basis_matrix, eye) and np.array_equal(c.inverse_basis_matrix, eye)) else 0.0
     elif isinstance(c, Triangle_Collider):
         rec["type"] = N.TRIANGLE
         p[0:3] = _f3(c.centroid)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Diagnostic builds: each removes one cost from the trace kernels (images are wrong; timing only).
+set -e
+cd "$(dirname "$0")/../python-raytracer_amd/csrc"
+mkdir -p ../../build/abl
+for f in SHADOW POW TEX FB APPEND QSTORE; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -munsafe-fp-atomics \
+    -DRT_ABL_$f -o ../../build/abl/libsightpy_hip_$f.so rt_kernels.hip &
+done
+wait
+ls -la ../../build/abl

@@ -26,6 +26,10 @@ for step in "$@"; do
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     configs) for c in example3_1080p_d8 example4_4k_d6 cornell_800_s512; do run "bench_$c" 600 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline; done ;;
     occ) for o in 0 2 3 4; do run "bench_occ$o" 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --occupancy $o; done ;;
+    abl) for f in build/abl/libsightpy_hip_*.so; do n=$(basename $f .so); run "abl_${n#libsightpy_hip_}" 300 env SIGHTPY_HIP_LIB=$f python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline; done ;;
+    pmc_list) run pmc_list 120 rocprofv3 -L ;;
+    pmc_sq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_sq1 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+            run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
