@@ -96,8 +96,9 @@ typedef struct srt_collider {
 /*
  * Material parameter layout (p[]):
  *   GLOSSY     0-2 solid diffuse colour * diff_coeff (tex < 0), 3 diff_coeff, 4 a = 2/r^2 - 2,
- *              5 a + 2.0, 6 2.0*pi, 7 spec_coeff, 8-10 F0 of the reflection term (scene.n vs n)
- *              (the specular F0 depends on the ray's medium: srt_scene_desc.glossy_f0)
+ *              5 a + 2.0, 6 2.0*pi, 7 spec_coeff, 8-10 F0 of the reflection term (scene.n vs n),
+ *              11-13 specular F0 for medium 0 (= glossy_f0[m][0]; the specular F0 depends on the
+ *              ray's medium: srt_scene_desc.glossy_f0)
  *   REFRACTIVE (index of refraction = media[medium])
  *   THINFILM   0 thickness, 1 noise factor
  *   DIFFUSE    0-2 solid colour, 3 ambient_weight, 4 1 - ambient_weight

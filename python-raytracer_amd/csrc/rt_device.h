@@ -21,8 +21,10 @@
 // per-material waterfall) become scalar loads into SGPRs instead of per-lane loads into VGPRs.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define RT_RO __attribute__((address_space(4)))
+#define RT_LDS __attribute__((address_space(3)))
 #else
 #define RT_RO
+#define RT_LDS
 #endif
 
 #if defined(__HIPCC__)
@@ -155,7 +157,17 @@ struct SceneView {
     int ncol, nmat, ntex, nlights, nmedia, nimp;
     int nshadow;  // colliders flagged SRT_CF_SHADOW
     double ambient[3];
+    // texture lookup tables staged in LDS by the kernel (textures [0, nlut_lds)); the host
+    // harness leaves nlut_lds = 0 and reads the tables from the texture records
+    const RT_LDS double* lut_lds;
+    int nlut_lds;
 };
+
+// lut[b] of texture `tid` (LDS copy when staged)
+RT_HD double tex_lut(const SceneView& S, int tid, uint8_t b) {
+    if (tid < S.nlut_lds) return S.lut_lds[tid * 256 + b];
+    return S.tex[tid].lut[b];
+}
 
 // ---- ray/primitive intersection (returns distance; orientation through `o`) -----------------
 // sphere.py:26-52
@@ -349,7 +361,7 @@ RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err)
     return d3{u * T.repeat, v, u + v};
 #endif
     const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
-    return d3{T.lut[px[0]], T.lut[px[1]], T.lut[px[2]]};
+    return d3{tex_lut(S, tid, px[0]), tex_lut(S, tid, px[1]), tex_lut(S, tid, px[2])};
 }
 
 // Material.get_Normal (material.py:18-36): collider normal (or normal map) times orientation
@@ -360,7 +372,9 @@ RT_HD d3 shading_normal(const SceneView& S, const RT_RO srt_collider& c, const R
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
         const RT_RO srt_texture& T = S.tex[m.normalmap];
         const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
-        d3 nm = d3{(T.lut[px[0]] - 0.5) * 2.0, (T.lut[px[1]] - 0.5) * 2.0, (T.lut[px[2]] - 0.5) * 2.0};
+        const int nmt = m.normalmap;
+        d3 nm = d3{(tex_lut(S, nmt, px[0]) - 0.5) * 2.0, (tex_lut(S, nmt, px[1]) - 0.5) * 2.0,
+                   (tex_lut(S, nmt, px[2]) - 0.5) * 2.0};
         const RT_RO double* ib = (c.type == SRT_PLANE) ? c.p + 16 : c.p + 30;
         return mul(normalize(matmul_rows(ib, nm)), orient);
     }
@@ -571,7 +585,8 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
         }
         color = add(color, mul(mul(diff, lv), seelight));
         if (m.flags & SRT_MF_ROUGH) {
-            d3 F0 = ld3(S.glossy_f0 + ((int64_t)mi * S.nmedia + med) * 3);
+            // medium 0 (scene.n, nearly every ray) has its F0 in the material record (scalar loads)
+            d3 F0 = (med == 0) ? ld3(m.p + 11) : ld3(S.glossy_f0 + ((int64_t)mi * S.nmedia + med) * 3);
             double cos_t = np_clip(dot(V, H), 0.0, 1.0);
             d3 F = schlick(F0, cos_t);
 #ifdef RT_ABL_POW  // diagnostic build only
@@ -669,14 +684,15 @@ RT_HD void shade_thinfilm(const SceneView& S, const RT_RO srt_collider& c, int m
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
         const RT_RO srt_texture& nt = S.tex[m.tex_aux1];
-        double nz = nt.lut[*tex_uv(S, nt, u, v, err)];
+        double nz = tex_lut(S, m.tex_aux1, *tex_uv(S, nt, u, v, err));
         double thick = m.p[0] + m.p[1] * (nz - 0.5);
         ti = np_trunc(thick);
     } else {
         ti = (int64_t)m.p[0];
     }
     const RT_RO uint8_t* px = texel_at(S, lut, li, ti, err);
-    d3 F = d3{lut.lut[px[0]], lut.lut[px[1]], lut.lut[px[2]]};
+    const int lt = m.tex_aux0;
+    d3 F = d3{tex_lut(S, lt, px[0]), tex_lut(S, lt, px[1]), tex_lut(S, lt, px[2])};
     em.local(mul(ld3(S.ambient), F));
     uint32_t med = meta_medium(r.meta), dfl = meta_diffuse(r.meta);
     em.child(mkchild(add(P, mul(N, NUDGE)), reflect_dir(r.d, N), F, med, dfl, 1));
@@ -695,7 +711,9 @@ RT_HD void shade_sky(const SceneView& S, const RT_RO srt_collider& c, int mi, co
     if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP)) {
         const RT_RO srt_texture& L = S.tex[m.tex_aux0];
         const RT_RO uint8_t* px = tex_uv(S, L, u, v, err);
-        col = d3{col.x + m.p[0] * L.lut[px[0]], col.y + m.p[0] * L.lut[px[1]], col.z + m.p[0] * L.lut[px[2]]};
+        const int lm = m.tex_aux0;
+        col = d3{col.x + m.p[0] * tex_lut(S, lm, px[0]), col.y + m.p[0] * tex_lut(S, lm, px[1]),
+                 col.z + m.p[0] * tex_lut(S, lm, px[2])};
     }
     em.local(col);
 }

@@ -47,7 +47,8 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 constexpr int BLOCK = 256;
-constexpr int NSHARD = 16;  // queue shards: one append counter per shard (blocks b, b+16, ... share one)
+constexpr int NSHARD = 16;
+constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)  // queue shards: one append counter per shard (blocks b, b+16, ... share one)
 
 struct Queue {
     double *ox, *oy, *oz, *dx, *dy, *dz, *wr, *wg, *wb;
@@ -208,24 +209,33 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     int id = -1;
     if (active) id = nearest_hit(S, r.o, r.d, t, o, ties);
     if (hit_slot && active) *hit_slot = id;
-    const int mat = (id >= 0) ? S.col[id].material : -1;
     GpuEmit em{P, r, shard, 0u, &shadow, acc};
-    // waterfall over the materials present in the wave: material index and its parameters are
-    // wave-uniform inside each pass (scalar loads, uniform type switch)
-    uint64_t pending = __ballot(mat >= 0);
+#ifdef RT_ABL_NOSHADE  // diagnostic build only: raygen + nearest hit, no shading
+    if (id == 12345) em.local(d3{t, o, 0.0});
+    return;
+#endif
+    // waterfall over the colliders hit in this wave: inside each pass the collider index, and so
+    // its material and every table entry they reference, is wave-uniform (scalar loads into SGPRs,
+    // uniform branches); a wave usually sees one to three distinct colliders
+    uint64_t pending = __ballot(id >= 0);
     while (pending) {
         const int lead = __builtin_ctzll(pending);
-        const int m = __builtin_amdgcn_readfirstlane(__shfl(mat, lead));
-        const bool mine = (mat == m);
+        const int cu = __builtin_amdgcn_readfirstlane(__shfl(id, lead));
+        const bool mine = (id == cu);
         if (mine) {
-            const auto& c = S.col[id];
+            // re-derive the uniform index inside the branch: here id == cu on every active lane, and
+            // the compiler would otherwise substitute the per-lane id back into every table
+            // address (vector loads into VGPRs instead of scalar loads)
+            const int cs = __builtin_amdgcn_readfirstlane(id);
+            const auto& c = S.col[cs];
+            const int m = c.material;
             switch (S.mat[m].type) {
                 case SRT_GLOSSY:
                     if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy(S, c, m, r, t, o, em, err);
                     break;
                 case SRT_REFRACTIVE:
                     if (MATS & mat_bit(SRT_REFRACTIVE))
-                        shade_refractive(S, c, m, r, t, o, em, err, mc_uniform(P, r, id, 0));
+                        shade_refractive(S, c, m, r, t, o, em, err, mc_uniform(P, r, cs, 0));
                     break;
                 case SRT_THINFILM:
                     if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, m, r, t, o, em, err);
@@ -244,11 +254,12 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         pending &= ~__ballot(mine);
     }
     // colliders tied at the same distance are all shaded and their colours added (ray.py:131-146)
-    if (ties) {
+    if (__ballot(ties)) {
+        // wave-uniform collider loop (scalar table loads); lanes act on later colliders at t
         uint32_t round = 1;
-        for (int c = id + 1; c < S.ncol; ++c) {
+        for (int c = 0; c < S.ncol; ++c) {
             double oc;
-            if (collider_hit(S.col[c], r.o, r.d, oc) == t) {
+            if (ties && c > id && collider_hit(S.col[c], r.o, r.d, oc) == t) {
                 GpuEmit et{P, r, shard, round++, &shadow, acc};
                 shade_hit<MATS>(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(P, r, c, round - 1));
             }
@@ -259,9 +270,20 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
 // Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
 // (camera.py:51-85) and tracing it; the pixel's depth-0 colour is summed in registers and added to
 // the framebuffer once (no other thread touches the pixel during this launch).
+// Copy the first `nlut` texture lookup tables into LDS (dynamic shared memory) and point the
+// scene view at them: texel -> value becomes an LDS read instead of a dependent global load.
+__device__ __forceinline__ void stage_luts(TraceParams& P) {
+    extern __shared__ double lds_lut[];
+    const int n = P.S.nlut_lds;
+    for (int i = threadIdx.x; i < n * 256; i += BLOCK) lds_lut[i] = P.S.tex[i >> 8].lut[i & 255];
+    P.S.lut_lds = (const RT_LDS double*)lds_lut;
+    __syncthreads();
+}
+
 template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
-    const TraceParams& P = P0;
+    TraceParams P = P0;
+    stage_luts(P);
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
     uint32_t shadow = 0;
@@ -275,6 +297,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         const int grow = active ? P.rows[lr] : 0;
         const double xc = active ? P.cam.xs[col] : 0.0, yr = active ? P.cam.ys[grow] : 0.0;
         d3 acc = d3{0.0, 0.0, 0.0};
+        const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
+        // software pipeline: the next sample's uniforms are loaded while this sample is traced
+        double jn[4] = {0.0, 0.0, 0.0, 0.0};
+        if (active) primary_uniforms(P, 0, p, gpix, jn);
         for (int s = 0; s < P.spp; ++s) {
             Ray r;
             r.o = r.d = d3{0.0, 0.0, 0.0};
@@ -282,11 +308,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             r.meta = pack_meta(0, 0, 0);
             r.pix = p;
             r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
-            if (active) {
-                double j[4];
-                primary_uniforms(P, s, p, (uint32_t)grow * (uint32_t)P.cam.width + col, j);
-                primary_ray(P.cam, xc, yr, j, r.o, r.d);
-            }
+            const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
+            if (active && s + 1 < P.spp) primary_uniforms(P, s + 1, p, gpix, jn);
+            if (active) primary_ray(P.cam, xc, yr, j, r.o, r.d);
             int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
             trace_one<MATS>(P, r, active, shard, err, shadow, hs, &acc);
         }
@@ -304,7 +328,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
 // b % NSHARD.
 template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
-    const TraceParams& P = P0;
+    TraceParams P = P0;
+    stage_luts(P);
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
     uint32_t shadow = 0;
@@ -559,6 +584,8 @@ TraceParams base_params(srt_ctx* c, uint64_t seed) {
 // deepest depth index that can hold rays: max_ray_depth, +2 diffuse bounces without depth check
 int depth_cap(const srt_ctx* c) { return std::min(SRT_MAX_DEPTHS - 2, c->max_depth + 1 + (c->has_diffuse ? 2 : 0)); }
 
+size_t lut_bytes(const srt_ctx* c) { return (size_t)c->S.nlut_lds * 256 * sizeof(double); }
+
 int trace_grid(const srt_ctx* c) { return std::max(NSHARD, (c->max_blocks / NSHARD) * NSHARD); }
 
 int64_t depth_total(const uint32_t* cnt, int64_t seg) {
@@ -699,6 +726,8 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
         if (m.type == SRT_DIFFUSE) { fan = std::max(fan, std::max(1, (int)m.ival)); c->has_diffuse = 1; }
     }
     for (int k = 0; k < 3; ++k) S.ambient[k] = d->ambient[k];
+    S.lut_lds = nullptr;
+    S.nlut_lds = std::min(d->n_textures, MAX_LUT_LDS);
     c->S = S;
     c->max_depth = std::max(0, (int)d->max_ray_depth);
     c->fanout = fan;
@@ -793,7 +822,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         P.cnt_out = c->counts + NSHARD;
         HIP_TRY(hipEventRecord(c->ev[0], c->stream));
         const Variant& V = pick_variant(c->mats);
-        hipLaunchKernelGGL(V.primary, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, P);
+        hipLaunchKernelGGL(V.primary, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), lut_bytes(c), c->stream,
+                           P);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev[1], c->stream));
         for (int d = 1; d <= dcap; ++d) {
@@ -802,7 +832,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.qout = c->q[(d + 1) & 1];
             P.cnt_in = c->counts + (int64_t)d * NSHARD;
             P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
+            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(c->ev[1 + d], c->stream));
         }
@@ -915,7 +945,7 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
             P.qout = c->q[(d + 1) & 1];
             P.cnt_in = c->counts + (int64_t)d * NSHARD;
             P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), 0, c->stream, P);
+            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream, P);
             HIP_TRY(hipGetLastError());
         }
         uint32_t flags[2];

@@ -266,6 +266,7 @@ def lower_scene(scene, extra_media=()):
             p[8:11] = _f3(F0)
             for k, arrs in enumerate(media_arrays):
                 glossy_f0[i, k] = _medium_f0(arrs, [m.n.x, m.n.y, m.n.z])
+            p[11:14] = glossy_f0[i, 0]  # medium 0 copy, read with scalar loads
         elif isinstance(m, Refractive):
             r["type"] = N.REFRACTIVE
             r["medium"] = medium_of(_c(m.n))
