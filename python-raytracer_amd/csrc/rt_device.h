@@ -12,6 +12,7 @@
 #pragma once
 
 #include <math.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/sightpy_rt.h"
@@ -158,10 +159,17 @@ struct SceneView {
     int nshadow;  // colliders flagged SRT_CF_SHADOW
     double ambient[3];
     // texture lookup tables staged in LDS by the kernel (textures [0, nlut_lds)); the host
-    // harness leaves nlut_lds = 0 and reads the tables from the texture records
-    const RT_LDS double* lut_lds;
+    // harness leaves nlut_lds = 0 and reads the tables from the texture records.  An LDS pointer
+    // is 32-bit in device code and 64-bit on the host; the union keeps the struct (a kernel
+    // argument built by the host) the same layout on both sides.
+    union {
+        const RT_LDS double* lut_lds;
+        uint64_t lut_lds_bits_;
+    };
     int nlut_lds;
 };
+// the host builds SceneView/TraceParams and the device reads them: the layout must agree
+static_assert(sizeof(SceneView) == 144 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
 
 // lut[b] of texture `tid` (LDS copy when staged)
 RT_HD double tex_lut(const SceneView& S, int tid, uint8_t b) {
@@ -600,6 +608,9 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
         }
     }
     em.local(color);
+#ifdef RT_ABL_NOEMIT  // diagnostic build only
+    return;
+#endif
     if ((int)meta_depth(r.meta) < c.max_ray_depth) {
         double cos_t = np_clip(dot(V, N), 0.0, 1.0);
         d3 F = schlick(ld3(m.p + 8), cos_t);
@@ -703,6 +714,10 @@ RT_HD void shade_thinfilm(const SceneView& S, const RT_RO srt_collider& c, int m
 template <class E>
 RT_HD void shade_sky(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, E& em,
                      uint32_t& err) {
+#ifdef RT_ABL_NOSKY  // diagnostic build only
+    em.local(d3{t, 0.5, 0.5});
+    return;
+#endif
     const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
     double u, v;

@@ -48,6 +48,7 @@ int fail(int code, const std::string& msg) {
 
 constexpr int BLOCK = 256;
 constexpr int NSHARD = 16;
+constexpr size_t TRACE_PARAMS_BYTES = 600;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)  // queue shards: one append counter per shard (blocks b, b+16, ... share one)
 
 struct Queue {
@@ -77,6 +78,9 @@ struct TraceParams {
     int spp;           // samples of this pass (k_primary)
     int32_t* hit_out;  // [spp][npix] or null
 };
+// kernel argument: host and device passes must agree on the layout (catches address-space pointer
+// size differences, see SceneView)
+static_assert(sizeof(TraceParams) == TRACE_PARAMS_BYTES, "TraceParams layout");
 
 __device__ __forceinline__ void queue_store(const Queue& q, int64_t i, d3 o, d3 d, d3 w, uint32_t pix,
                                             uint32_t meta, uint32_t path) {
@@ -123,6 +127,9 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t cnt) {
         below += lanes_below(m) << b;
     }
     uint32_t base = 0;
+#ifdef RT_ABL_NOATOMIC  // diagnostic build only: no counter traffic at all
+    return below + (total & 0u);
+#endif
 #ifdef RT_ABL_APPEND  // diagnostic build only: counts kept, slots not waited for (wrong images)
     if (lanes_below(__ballot(1)) == 0) atomicAdd(ctr, total);
     return ((blockIdx.x * 256u + threadIdx.x) * 2u + below % 2u) % 400000u;
@@ -150,7 +157,7 @@ struct GpuEmit {
     }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void store(uint32_t slot, const Child& c, uint32_t path) const {
-#ifdef RT_ABL_QSTORE  // diagnostic build only: no queue stores
+#if defined(RT_ABL_QSTORE) || defined(RT_ABL_NOATOMIC)  // diagnostic build only: no queue stores
         if (c.o.x == 12345.678) P.flags[1] = path;
         return;
 #endif

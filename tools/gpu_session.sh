@@ -14,6 +14,8 @@ run() {
   local rc=$?
   echo "$name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a gpurun_out/summary.txt
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  # a failed smoke test means the library is broken: run nothing else on the GPU
+  if [ $rc -ne 0 ] && [ "$name" = smoke ]; then echo "stopping after failed smoke"; exit $rc; fi
 }
 for step in "$@"; do
   case $step in
