@@ -41,11 +41,6 @@ CONFIGS = {
 }
 
 
-def shard_rows(height, world, rank, band=8):
-    rows = np.arange(height)
-    return rows[(rows // band) % world == rank]
-
-
 def cpu_baseline(builder, W, H, depth, spp, budget_s=20.0):
     """Oracle (numpy port of the reference algorithm) timed on this host's CPU, one process, on the
     same frame: samples are traced one after another until the frame is done or `budget_s` of CPU
@@ -112,6 +107,7 @@ def main():
 
     import scenes
     from sightpy import _backend as B, _native as N
+    from sightpy._shard import shard_rows, gather_rows
 
     builder, W, H, depth, spp, label = CONFIGS[args.config]
     if args.spp:
@@ -147,21 +143,20 @@ def main():
     a.seed = 12345
     a.out_rgb, a.out_srgb8, a.out_hit_id = out_rgb, out_u8, None
 
-    gather = None
+    tile = None
     if dist is not None:
         import torch
 
-        maxrows = max(len(shard_rows(H, world, r)) for r in range(world))
-        tile = torch.zeros(maxrows * W * 3, dtype=torch.uint8, device="cuda")
-        gather = (torch, tile, torch.empty(world * maxrows * W * 3, dtype=torch.uint8, device="cuda"))
+        tile = torch.zeros((len(rows), W, 3), dtype=torch.uint8, device="cuda")
+    frame = {}
 
     def step(st):
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
-        if gather is not None:
-            torch, tile, full = gather
-            # rank tile -> torch buffer (device to device), then RCCL all-gather over xGMI
+        if tile is not None:
+            # rank tile -> torch buffer (device to device; srt_memcpy synchronises the library's
+            # stream), then one RCCL all-gather over xGMI and the row un-permutation on device
             N.check(lib, lib.srt_memcpy(ctx, ctypes.c_void_p(tile.data_ptr()), out_u8, 3 * npix))
-            dist.all_gather_into_tensor(full, tile)
+            frame["image"] = gather_rows(tile, H, world)
 
     st = N.Stats()
     for _ in range(args.warmup):

@@ -182,6 +182,8 @@ class TraceArgs(ctypes.Structure):
 
 
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
+ABI_VERSION = 1  # SRT_ABI_VERSION of include/sightpy_rt.h
+
 SIGNATURES = {
     "srt_abi_version": (ctypes.c_int, []),
     "srt_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
@@ -227,7 +229,7 @@ def load_library(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.srt_abi_version() != 1:
+    if lib.srt_abi_version() != ABI_VERSION:
         raise BackendUnavailable("ABI version mismatch in %s" % path)
     return lib
 

@@ -1,0 +1,58 @@
+"""Row-band sharding of a frame across ranks (one process per GPU) and the final gather.
+
+The reference parallelises `Scene.render` over samples with `multiprocessing.Pool`
+(`sightpy/scene.py:80-116`).  Pixels are independent, so here the frame is split instead: rank r
+owns the rows `{y : (y // band) % world == r}` (bands dealt round-robin, which balances the cheap
+sky rows against the reflective floor rows), renders them with the same per-pixel jitter the
+single-GPU render would use, and the uint8 tiles are all-gathered (`torch.distributed`; backend
+`nccl` = RCCL over xGMI on MI355X, `gloo` on CPU for tests).  The assembled image is independent of
+the number of ranks.
+"""
+import numpy as np
+
+BAND = 8
+
+
+def shard_rows(height, world, rank, band=BAND):
+    """Image rows owned by `rank` (ascending)."""
+    rows = np.arange(int(height))
+    return rows[(rows // band) % world == rank]
+
+
+def max_shard_rows(height, world, band=BAND):
+    """Largest per-rank row count (the padded tile height of the gather)."""
+    return max(len(shard_rows(height, world, r, band)) for r in range(world))
+
+
+def assemble_index(height, world, band=BAND):
+    """For every image row, its position in the gathered buffer of padded tiles:
+    `gathered.reshape(world * maxrows, ...)[idx]` is the image."""
+    maxrows = max_shard_rows(height, world, band)
+    idx = np.empty(int(height), dtype=np.int64)
+    for r in range(world):
+        rows = shard_rows(height, world, r, band)
+        idx[rows] = r * maxrows + np.arange(len(rows))
+    return idx
+
+
+def gather_rows(tile, height, world, group=None, band=BAND):
+    """All-gather each rank's row tile and return the full image on every rank.
+
+    `tile` is a torch tensor of shape (len(shard_rows(...)), ...) on the collective's device
+    (cuda for nccl, cpu for gloo).  Tiles are padded to the largest shard so a single
+    `all_gather_into_tensor` (one RCCL collective) moves the frame."""
+    import torch
+    import torch.distributed as dist
+
+    maxrows = max_shard_rows(height, world, band)
+    rest = tuple(tile.shape[1:])
+    padded = tile.new_zeros((maxrows,) + rest)
+    padded[: tile.shape[0]] = tile
+    full = tile.new_empty((world * maxrows,) + rest)
+    if dist.get_backend(group) == "gloo":
+        # gloo has no all_gather_into_tensor; gather into views of the same buffer
+        dist.all_gather(list(full.chunk(world)), padded, group=group)
+    else:
+        dist.all_gather_into_tensor(full, padded, group=group)
+    idx = torch.as_tensor(assemble_index(height, world, band), device=full.device)
+    return full.index_select(0, idx)

@@ -75,10 +75,27 @@ class Scene:
             self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
         elif rng != "device":
             raise ValueError("rng must be 'numpy' or 'device'")
-        out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size)
+        world, rank = _dist_world()
+        if world == 1:
+            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size)
+            srgb8 = out.srgb8
+        else:
+            # one process per GPU under torch.distributed: render this rank's row bands, gather
+            import torch
+            from ._shard import shard_rows, gather_rows
+
+            H, W = int(self.camera.screen_height), int(self.camera.screen_width)
+            rows = shard_rows(H, world, rank)
+            if jitter is not None:
+                jitter = jitter.reshape(samples_per_pixel, 4, H, W)[:, :, rows].reshape(samples_per_pixel, 4, -1)
+            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size, rows=rows)
+            tile = torch.from_numpy(out.srgb8)
+            if torch.distributed.get_backend() == "nccl":
+                tile = tile.cuda()
+            srgb8 = gather_rows(tile, H, world).cpu().numpy()
         self.last_stats = out.stats
         print("Render Took", time.time() - t0)
-        return Image.fromarray(out.srgb8, "RGB")
+        return Image.fromarray(srgb8, "RGB")
 
     def get_distances(self):
         """Grey depth map of one primary sample (reference scene.py:142-166)."""
@@ -94,6 +111,19 @@ class Scene:
         h, w = self.camera.screen_height, self.camera.screen_width
         u8 = (255 * np.clip(g, 0, 1).reshape((h, w))).astype(np.uint8)
         return Image.fromarray(np.stack([u8, u8, u8], axis=-1), "RGB")
+
+
+def _dist_world():
+    """(world size, rank) of an initialised torch.distributed job, else (1, 0)."""
+    import sys
+
+    if "torch.distributed" not in sys.modules:
+        return 1, 0
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1, 0
+    return dist.get_world_size(), dist.get_rank()
 
 
 def get_raycolor_tuple(x):
