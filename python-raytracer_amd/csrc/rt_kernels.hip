@@ -75,6 +75,7 @@ struct TraceParams {
     int64_t seg;             // capacity of one queue shard (rays)
     uint64_t seed;
     int depth;
+    int fb_first;  // depth 0 of the first pass: store the pixel instead of adding (no memset)
     // primary generation
     int64_t n_primary;
     srt_camera cam;
@@ -327,7 +328,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
             trace_one<MATS>(P, r, active, shard, err, shadow, hs, &acc);
         }
-        if (active && !is_zero(acc)) {
+        if (active && P.fb_first) {
+            P.fb[p] = acc.x;
+            P.fb[P.npix + p] = acc.y;
+            P.fb[2 * P.npix + p] = acc.z;
+        } else if (active && !is_zero(acc)) {
             P.fb[p] += acc.x;
             P.fb[P.npix + p] += acc.y;
             P.fb[2 * P.npix + p] += acc.z;
@@ -503,6 +508,7 @@ struct srt_ctx {
     double* ys = nullptr;
     int32_t* rows = nullptr;
     int64_t cam_cap[3] = {0, 0, 0};
+    std::vector<uint8_t> cam_host[3];  // host copies of what xs / ys / rows hold
     double* jit = nullptr;
     int64_t jit_cap = 0;
     int32_t* hit = nullptr;
@@ -511,6 +517,8 @@ struct srt_ctx {
     uint32_t* flags = nullptr;   // [2]
     unsigned long long* shadow = nullptr;
     std::vector<hipEvent_t> ev;
+    uint32_t* host = nullptr;  // pinned: per-pass counters/flags, shadow count
+    int64_t host_words = 0;
 };
 
 namespace {
@@ -595,11 +603,27 @@ TraceParams base_params(srt_ctx* c, uint64_t seed) {
 }
 
 // deepest depth index that can hold rays: max_ray_depth, +2 diffuse bounces without depth check
-int depth_cap(const srt_ctx* c) { return std::min(SRT_MAX_DEPTHS - 2, c->max_depth + 1 + (c->has_diffuse ? 2 : 0)); }
+// (a child is made only while depth < max_ray_depth, so depth max_ray_depth is the last with rays;
+// Diffuse bounces ignore max_ray_depth (diffuse.py:25-124) and add at most two more)
+int depth_cap(const srt_ctx* c) { return std::min(SRT_MAX_DEPTHS - 2, c->max_depth + (c->has_diffuse ? 2 : 0)); }
 
 size_t lut_bytes(const srt_ctx* c) { return (size_t)c->S.nlut_lds * 256 * sizeof(double); }
 
 int trace_grid(const srt_ctx* c) { return std::max(NSHARD, (c->max_blocks / NSHARD) * NSHARD); }
+
+// copy `bytes` from host `src` to device `dst` unless `shadow` (the host copy of what dst holds)
+// already equals it.  The shadow is invalidated whenever the buffer is reallocated (ensure_buf).
+int upload_if_changed(srt_ctx* c, void* dst, std::vector<uint8_t>& shadow, const void* src, size_t bytes) {
+    if (is_device_ptr(src)) {
+        shadow.clear();
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+        return SRT_OK;
+    }
+    if (shadow.size() == bytes && !memcmp(shadow.data(), src, bytes)) return SRT_OK;
+    shadow.assign((const uint8_t*)src, (const uint8_t*)src + bytes);
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return SRT_OK;
+}
 
 int64_t depth_total(const uint32_t* cnt, int64_t seg) {
     int64_t t = 0;
@@ -654,6 +678,7 @@ int srt_destroy(srt_ctx* c) {
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+    if (c->host) (void)hipHostFree(c->host);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SRT_OK;
@@ -771,13 +796,20 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     const int64_t npix = (int64_t)a->n_rows * W;
     if (npix >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "image too large");
     int rc;
-    if ((rc = ensure_buf(&c->xs, c->cam_cap[0], W))) return rc;
-    if ((rc = ensure_buf(&c->ys, c->cam_cap[1], cam->height))) return rc;
-    if ((rc = ensure_buf(&c->rows, c->cam_cap[2], a->n_rows))) return rc;
-    HIP_TRY(hipMemcpyAsync(c->xs, cam->xs, W * 8, hipMemcpyDefault, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->ys, cam->ys, (size_t)cam->height * 8, hipMemcpyDefault, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->rows, a->rows ? a->rows : rows_h.data(), (size_t)a->n_rows * 4, hipMemcpyDefault,
-                           c->stream));
+    {
+        const void* old[3] = {c->xs, c->ys, c->rows};
+        if ((rc = ensure_buf(&c->xs, c->cam_cap[0], W))) return rc;
+        if ((rc = ensure_buf(&c->ys, c->cam_cap[1], cam->height))) return rc;
+        if ((rc = ensure_buf(&c->rows, c->cam_cap[2], a->n_rows))) return rc;
+        const void* now[3] = {c->xs, c->ys, c->rows};
+        for (int k = 0; k < 3; ++k)
+            if (old[k] != now[k]) c->cam_host[k].clear();
+    }
+    // camera tables: uploaded only when they change (a render loop re-sends the same ones)
+    if ((rc = upload_if_changed(c, c->xs, c->cam_host[0], cam->xs, (size_t)W * 8))) return rc;
+    if ((rc = upload_if_changed(c, c->ys, c->cam_host[1], cam->ys, (size_t)cam->height * 8))) return rc;
+    if ((rc = upload_if_changed(c, c->rows, c->cam_host[2], a->rows ? a->rows : rows_h.data(), (size_t)a->n_rows * 4)))
+        return rc;
     if ((rc = ensure_buf(&c->fb, c->fb_cap, 3 * npix))) return rc;
     if ((rc = ensure_buf(&c->rgb, c->rgb_cap, 3 * npix))) return rc;
     if ((rc = ensure_buf(&c->u8, c->u8_cap, 3 * npix))) return rc;
@@ -792,118 +824,133 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     if (a->jitter && !jit_dev && (rc = ensure_buf(&c->jit, c->jit_cap, (int64_t)batch * 4 * npix))) return rc;
     const bool hit_dev = is_device_ptr(a->out_hit_id);
     if (a->out_hit_id && !hit_dev && (rc = ensure_buf(&c->hit, c->hit_cap, (int64_t)batch * npix))) return rc;
+    if ((rc = ensure_queues(c, (int64_t)batch * npix * c->fanout))) return rc;
     const int dcap = depth_cap(c);
-    if ((int)c->ev.size() < dcap + 2) {
+    const int npass = (a->spp + batch - 1) / batch;
+    const int nev = dcap + 2;  // events per pass: before k_primary, after each depth
+    if ((int)c->ev.size() < npass * nev) {
         for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-        c->ev.assign(dcap + 2, nullptr);
+        c->ev.assign(npass * nev, nullptr);
         for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
     }
-    if ((rc = ensure_queues(c, (int64_t)batch * npix * c->fanout))) return rc;
+    // per-pass counters and flags come back through pinned memory once, at the end of the frame:
+    // the passes, the resolve and the output copies are queued without a host round trip
+    const int64_t cnt_words = (int64_t)SRT_MAX_DEPTHS * NSHARD;
+    const int64_t pass_words = cnt_words + 2;
+    if (c->host_words < npass * pass_words + 2) {
+        if (c->host) (void)hipHostFree(c->host);
+        c->host = nullptr;
+        c->host_words = 0;
+        HIP_TRY(hipHostMalloc((void**)&c->host, (size_t)(npass * pass_words + 2) * 4, hipHostMallocDefault));
+        c->host_words = npass * pass_words + 2;
+    }
     srt_stats S{};
-    HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * npix * 8, c->stream));
-    HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
-    double ms_trace = 0.0, ms_primary = 0.0, ms_device = 0.0;
-    std::vector<uint32_t> counts(SRT_MAX_DEPTHS * NSHARD);
-    for (int s0 = 0; s0 < a->spp;) {
-        const int ns = std::min(batch, a->spp - s0);
-        const int64_t nrays = (int64_t)ns * npix;
-        HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->stream));
-        HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
-        TraceParams P = base_params(c, a->seed);
-        P.fb = c->fb;
-        P.npix = npix;
-        P.cam = *cam;
-        P.cam.xs = c->xs;
-        P.cam.ys = c->ys;
-        P.rows = c->rows;
-        P.sample_base = a->sample_base + s0;
-        P.spp = ns;
-        if (a->jitter) {
-            const double* src = a->jitter + (int64_t)s0 * 4 * npix;
-            if (jit_dev) {
-                P.jitter = src;
-            } else {
-                HIP_TRY(hipMemcpyAsync(c->jit, src, (size_t)nrays * 4 * 8, hipMemcpyHostToDevice, c->stream));
-                P.jitter = c->jit;
+    const Variant& V = pick_variant(c->mats);
+    for (;;) {
+        HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
+        for (int p = 0; p < npass; ++p) {
+            const int s0 = p * batch;
+            const int ns = std::min(batch, a->spp - s0);
+            const int64_t nrays = (int64_t)ns * npix;
+            HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)cnt_words * 4, c->stream));
+            HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
+            TraceParams P = base_params(c, a->seed);
+            P.fb = c->fb;
+            P.fb_first = (p == 0);  // the first pass's depth-0 kernel stores the framebuffer (no memset)
+            P.npix = npix;
+            P.cam = *cam;
+            P.cam.xs = c->xs;
+            P.cam.ys = c->ys;
+            P.rows = c->rows;
+            P.sample_base = a->sample_base + s0;
+            P.spp = ns;
+            if (a->jitter) {
+                const double* src = a->jitter + (int64_t)s0 * 4 * npix;
+                if (jit_dev) {
+                    P.jitter = src;
+                } else {
+                    HIP_TRY(hipMemcpyAsync(c->jit, src, (size_t)nrays * 4 * 8, hipMemcpyHostToDevice, c->stream));
+                    P.jitter = c->jit;
+                }
             }
-        }
-        if (a->out_hit_id) P.hit_out = hit_dev ? a->out_hit_id + (int64_t)s0 * npix : c->hit;
-        // depth 0: raygen fused with the trace step
-        P.depth = 0;
-        P.n_primary = nrays;
-        P.qout = c->q[1];
-        P.cnt_out = c->counts + NSHARD;
-        HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-        const Variant& V = pick_variant(c->mats);
-        hipLaunchKernelGGL(V.primary, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), lut_bytes(c), c->stream,
-                           P);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-        for (int d = 1; d <= dcap; ++d) {
-            P.depth = d;
-            P.qin = c->q[d & 1];
-            P.qout = c->q[(d + 1) & 1];
-            P.cnt_in = c->counts + (int64_t)d * NSHARD;
-            P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream, P);
+            if (a->out_hit_id) P.hit_out = hit_dev ? a->out_hit_id + (int64_t)s0 * npix : c->hit;
+            hipEvent_t* ev = c->ev.data() + (int64_t)p * nev;
+            // depth 0: raygen fused with the trace step
+            P.depth = 0;
+            P.n_primary = nrays;
+            P.qout = c->q[1];
+            P.cnt_out = c->counts + NSHARD;
+            HIP_TRY(hipEventRecord(ev[0], c->stream));
+            hipLaunchKernelGGL(V.primary, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), lut_bytes(c), c->stream,
+                               P);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(c->ev[1 + d], c->stream));
+            HIP_TRY(hipEventRecord(ev[1], c->stream));
+            P.fb_first = 0;
+            for (int d = 1; d <= dcap; ++d) {
+                P.depth = d;
+                P.qin = c->q[d & 1];
+                P.qout = c->q[(d + 1) & 1];
+                P.cnt_in = c->counts + (int64_t)d * NSHARD;
+                P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
+                hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream, P);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipEventRecord(ev[1 + d], c->stream));
+            }
+            uint32_t* hp = c->host + p * pass_words;
+            HIP_TRY(hipMemcpyAsync(hp, c->counts, (size_t)cnt_words * 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(hp + cnt_words, c->flags, 8, hipMemcpyDeviceToHost, c->stream));
+            if (a->out_hit_id && !hit_dev)
+                HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->hit, (size_t)nrays * 4,
+                                       hipMemcpyDeviceToHost, c->stream));
         }
-        uint32_t flags[2];
-        HIP_TRY(hipMemcpyAsync(counts.data(), c->counts, counts.size() * 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(flags, c->flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
-        if (a->out_hit_id && !hit_dev)
-            HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->hit, (size_t)nrays * 4,
-                                   hipMemcpyDeviceToHost, c->stream));
+        hipLaunchKernelGGL(k_resolve, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb, npix,
+                           0.0, (double)a->spp, c->rgb, c->u8);
+        HIP_TRY(hipGetLastError());
+        if (a->out_rgb)
+            HIP_TRY(hipMemcpyAsync(a->out_rgb, c->rgb, (size_t)3 * npix * 8, hipMemcpyDefault, c->stream));
+        if (a->out_srgb8) HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->u8, (size_t)3 * npix, hipMemcpyDefault, c->stream));
+        uint32_t* hshadow = c->host + npass * pass_words;
+        HIP_TRY(hipMemcpyAsync(hshadow, c->shadow, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if ((rc = check_flags(flags[0]))) return rc;
-        if (flags[1]) {
-            // a queue shard overflowed: grow and restart the frame (this pass's sum is partial)
+        bool overflow = false;
+        for (int p = 0; p < npass; ++p) {
+            const uint32_t* hp = c->host + p * pass_words;
+            if ((rc = check_flags(hp[cnt_words]))) return rc;
+            overflow |= hp[cnt_words + 1] != 0;
+        }
+        if (overflow) {
+            // a queue shard overflowed: grow the queues and render the frame again
             S.retries++;
             if (S.retries > 8) return fail(SRT_ERR_MEMORY, "ray queues keep overflowing");
             if ((rc = ensure_queues(c, 2 * c->seg * NSHARD))) return rc;
-            HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * npix * 8, c->stream));
-            HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
-            s0 = 0;
-            for (auto& v : S.rays_per_depth) v = 0;
-            ms_trace = ms_primary = ms_device = 0.0;
-            S.passes = 0;
             continue;
         }
-        if (depth_total(counts.data() + (int64_t)(dcap + 1) * NSHARD, c->seg) != 0)
-            return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
-        S.rays_per_depth[0] += nrays;
-        for (int d = 1; d <= dcap; ++d) S.rays_per_depth[d] += depth_total(counts.data() + (int64_t)d * NSHARD, c->seg);
-        float ms;
-        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-        ms_primary += ms;
-        ms_trace += ms;
-        for (int d = 1; d <= dcap; ++d) {
-            HIP_TRY(hipEventElapsedTime(&ms, c->ev[d], c->ev[d + 1]));
+        double ms_trace = 0.0, ms_primary = 0.0, ms_device = 0.0;
+        for (int p = 0; p < npass; ++p) {
+            const uint32_t* hp = c->host + p * pass_words;
+            if (depth_total(hp + (int64_t)(dcap + 1) * NSHARD, c->seg) != 0)
+                return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
+            S.rays_per_depth[0] += (int64_t)std::min(batch, a->spp - p * batch) * npix;
+            for (int d = 1; d <= dcap; ++d) S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, c->seg);
+            const hipEvent_t* ev = c->ev.data() + (int64_t)p * nev;
+            float ms;
+            HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+            ms_primary += ms;
+            HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[dcap + 1]));
             ms_trace += ms;
+            ms_device += ms;
         }
-        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[dcap + 1]));
-        ms_device += ms;
-        S.passes++;
-        s0 += ns;
+        S.passes = npass;
+        S.ms_trace_kernels = ms_trace;
+        S.ms_primary_kernel = ms_primary;
+        S.ms_device = ms_device;
+        S.shadow_rays = (int64_t)(hshadow[0] | (uint64_t)hshadow[1] << 32);
+        break;
     }
-    hipLaunchKernelGGL(k_resolve, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb, npix, 0.0,
-                       (double)a->spp, c->rgb, c->u8);
-    HIP_TRY(hipGetLastError());
-    if (a->out_rgb)
-        HIP_TRY(hipMemcpyAsync(a->out_rgb, c->rgb, (size_t)3 * npix * 8, hipMemcpyDefault, c->stream));
-    if (a->out_srgb8) HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->u8, (size_t)3 * npix, hipMemcpyDefault, c->stream));
-    unsigned long long shadow = 0;
-    HIP_TRY(hipMemcpyAsync(&shadow, c->shadow, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     if (st) {
         S.n_depths = dcap + 1;
         S.total_rays = 0;
         for (int d = 0; d <= dcap; ++d) S.total_rays += S.rays_per_depth[d];
-        S.shadow_rays = (int64_t)shadow;
-        S.ms_trace_kernels = ms_trace;
-        S.ms_primary_kernel = ms_primary;
-        S.ms_device = ms_device;
         S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         *st = S;
     }
