@@ -69,6 +69,20 @@ def cpu_baseline(builder, W, H, depth, spp, budget_s=20.0):
             "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
 
 
+def pmc_traffic(config):
+    """HBM bytes per k_primary launch from the newest committed PMC summary of this config
+    (profiles/rNN_traffic_<config>.json, written by tools/pmc_traffic.py from two separate
+    rocprofv3 --pmc passes of this same bench command), or None."""
+    files = sorted(ROOT.glob("profiles/r*_traffic_%s.json" % config))
+    if not files:
+        return None, None
+    rec = json.loads(files[-1].read_text())
+    for name, k in rec["kernels"].items():
+        if "k_primary" in name and "traffic_bytes" in k:
+            return k["traffic_bytes"] / 1e9, files[-1].name
+    return None, None
+
+
 def _cpu_model():
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
@@ -198,6 +212,7 @@ def main():
     rpd = stats[0]["rays_per_depth"]
     achieved = rpd[0] * BYTES_PER_RAY / (prim_ms * 1e-3) / 1e9
     family = stats[0]["total_rays"] * BYTES_PER_RAY / (trace_ms * 1e-3) / 1e9
+    traffic_gb, traffic_src = pmc_traffic(args.config)
     if rank == 0:
         rec = {
             "metric": "Mrays/sec (primary+secondary) at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
@@ -217,9 +232,13 @@ def main():
                        "rays_per_frame": int(total_rays), "rays_per_depth_rank0": rpd,
                        "shadow_rays_rank0": stats[0]["shadow_rays"], "parallelism": "row-band shards x%d" % world,
                        "frame_ms": round(ms_step, 4)},
-            "roofline": {"bound": "hbm", "kernel": "k_trace<true> (depth-0 raygen+trace)",
+            "roofline": {"bound": "hbm", "kernel": "k_primary (depth 0: raygen + nearest hit + shading, fused)",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic_gb is None else round(traffic_gb, 4),
+                         "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_GB_per_launch": round(rpd[0] * BYTES_PER_RAY / 1e9, 4),
                          "bytes_per_ray": BYTES_PER_RAY, "kernel_ms": round(float(prim_ms), 4),
                          "all_trace_kernels": {"ms": round(float(trace_ms), 4), "achieved_GBs": round(family, 2),
                                                "frac": round(family / HBM_PEAK_GBS, 4)}},
