@@ -155,6 +155,24 @@ def gen_examples(sp, only=None):
         print(name, "rays per depth", counts.tolist(), "rgb mean", lin.mean())
 
 
+FEATURE_CONFIGS = [
+    # name, W, H, depth, spp, seed: tests/scenes.py:features built with the reference's module
+    ("features_64x48_d4_s2", 64, 48, 4, 2, 0),
+]
+
+
+def gen_features(sp):
+    sys.path.insert(0, str(OUT.parent))
+    import scenes
+
+    for name, W, H, depth, spp, seed in FEATURE_CONFIGS:
+        scene = scenes.features(W, H, depth, sp=sp)
+        lin, u8, hits, nears, counts = render_golden(sp, scene, spp, seed)
+        np.savez_compressed(OUT / (name + ".npz"), rgb=lin, srgb8=u8, hit_id=hits.astype(np.int16), nearest=nears,
+                            depth_counts=counts, seed=seed, spp=spp, width=W, height=H, depth=depth)
+        print(name, "rays per depth", counts.tolist(), "rgb mean", lin.mean())
+
+
 def gen_colliders(sp):
     """Known-answer tests of every collider's intersect on random and edge-case rays."""
     from sightpy.geometry.triangle import Triangle_Collider
@@ -238,4 +256,8 @@ if __name__ == "__main__":
         gen_camera(sp)
     if not only or "textures" in only:
         gen_textures(sp)
-    gen_examples(sp, [o for o in only if o not in ("colliders", "camera", "textures")] or None)
+    if not only or "features" in only:
+        gen_features(sp)
+    rest = [o for o in only if o not in ("colliders", "camera", "textures", "features")]
+    if not only or rest:
+        gen_examples(sp, rest or None)

@@ -119,3 +119,41 @@ def cornell(width=100, height=100, depth=None):
 
 BUILDERS = {"example1": example1, "example2": example2, "example3": example3, "example4": example4,
             "cornell": cornell}
+
+
+def features(width=64, height=48, depth=4, sp=None):
+    """Feature scene (not one of the reference's scripts): exercises the API paths the examples do
+    not reach -- normal map on a textured floor (material.py:18-40), a rotated textured Cuboid
+    (cuboid.py:84-187 uv cross), an absorbing glass sphere, an Emissive sphere, a metal with
+    roughness, two directional lights and a spherical Panorama background (panorama.py:10-26).
+
+    `sp` is the sightpy module to build with: this package by default; tests/golden/gen_golden.py
+    passes the reference's module so the fixture comes from the reference itself."""
+    if sp is None:
+        import sightpy as sp
+    vec3, rgb = sp.vec3, sp.rgb
+    floor = sp.Glossy(diff_color=sp.image("checkered_floor.png", repeat=6.0), n=vec3(1.2 + 0.3j, 1.2 + 0.3j, 1.1 + 0.3j),
+                      roughness=0.3, spec_coeff=0.4, diff_coeff=0.9)
+    floor.set_normalmap("floor.jpg", repeat=4.0)
+    wood = sp.Glossy(diff_color=sp.image("wood.jpg"), n=vec3(1.5 + 0j, 1.5 + 0j, 1.5 + 0j), roughness=0.5,
+                     spec_coeff=0.2, diff_coeff=0.8)
+    glass = sp.Refractive(n=vec3(1.5 + 4e-8j, 1.5 + 1e-8j, 1.5 + 0j))
+    metal = sp.Glossy(diff_color=rgb(0.8, 0.7, 0.3), n=vec3(0.2 + 3.0j, 0.5 + 2.5j, 1.3 + 2.0j), roughness=0.15,
+                      spec_coeff=0.6, diff_coeff=0.2)
+    lamp = sp.Emissive(color=rgb(3.0, 2.5, 2.0))
+    sc = sp.Scene(ambient_color=rgb(0.05, 0.05, 0.05))
+    sc.add_Camera(look_from=vec3(0.5, 1.2, 3.0), look_at=vec3(0.0, 0.1, -1.0), screen_width=width,
+                  screen_height=height)
+    sc.add_DirectionalLight(Ldir=vec3(0.5, 0.6, 0.4), color=rgb(0.6, 0.6, 0.55))
+    sc.add_DirectionalLight(Ldir=vec3(-0.7, 0.3, 0.2), color=rgb(0.2, 0.2, 0.3))
+    sc.add(sp.Plane(material=floor, center=vec3(0.0, -0.5, -1.0), width=20.0, height=20.0, u_axis=vec3(1.0, 0, 0),
+                    v_axis=vec3(0, 0, -1.0), max_ray_depth=depth))
+    cb = sp.Cuboid(material=wood, center=vec3(-1.0, 0.0, -1.2), width=0.8, height=1.0, length=0.6,
+                   max_ray_depth=depth, shadow=True)
+    cb.rotate(θ=25, u=vec3(0, 1, 0))
+    sc.add(cb)
+    sc.add(sp.Sphere(material=glass, center=vec3(0.6, 0.0, -0.8), radius=0.5, max_ray_depth=depth, shadow=False))
+    sc.add(sp.Sphere(material=metal, center=vec3(0.1, -0.25, 0.2), radius=0.25, max_ray_depth=depth))
+    sc.add(sp.Sphere(material=lamp, center=vec3(1.5, 0.8, -2.0), radius=0.3, max_ray_depth=depth, shadow=False))
+    sc.add_Background("miramar.jpeg", spherical=True)
+    return sc

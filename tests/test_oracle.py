@@ -97,6 +97,7 @@ DETERMINISTIC = [
     ("ex2_64x48_d3_s2", scenes.example2, None),
     ("ex3_64x48_d8_s2", scenes.example3, 8),
     ("ex4_48x36_d6_s1", scenes.example4, 6),
+    ("features_64x48_d4_s2", scenes.features, 4),
 ]
 
 
