@@ -100,8 +100,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
-    ap.add_argument("--rng", default="numpy", choices=["numpy", "device"],
-                    help="numpy: reference jitter stream resident in HBM; device: Philox raygen")
+    ap.add_argument("--rng", default="numpy", choices=["numpy", "device", "mt"],
+                    help="numpy: reference jitter stream resident in HBM; mt: the same stream generated on "
+                         "the GPU inside every step (srt_mt19937_uniforms); device: Philox raygen")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--occupancy", type=int, default=0, help="experiment: kernel variant with this waves/SIMD bound")
@@ -135,6 +136,17 @@ def main():
     npix = len(rows) * W
     # resident inputs: jitter (reference stream, seed 0) in HBM
     jit_dev = None
+    np.random.seed(0)
+    mt_state = np.random.get_state()
+    mt_key = np.ascontiguousarray(mt_state[1], dtype=np.uint32)
+    mt_key_out = np.empty(624, dtype=np.uint32)
+    mt_pos_out = ctypes.c_int32(0)
+    if args.rng == "mt" and world > 1:
+        raise SystemExit("--rng mt renders the full frame's stream; use it with --gpus 1")
+    if args.rng == "mt":
+        p = ctypes.c_void_p()
+        N.check(lib, lib.srt_device_alloc(ctx, spp * 4 * npix * 8, ctypes.byref(p)))
+        jit_dev = p
     if args.rng == "numpy":
         np.random.seed(0)
         jit = np.random.rand(spp * 4 * H * W).reshape(spp, 4, H, W)[:, :, rows].reshape(spp, 4, npix)
@@ -165,6 +177,10 @@ def main():
     frame = {}
 
     def step(st):
+        if args.rng == "mt":
+            # the reference's stream (seed 0): spp x 4 x npix jitter + the sizing draw, on the GPU
+            N.check(lib, lib.srt_mt19937_uniforms(ctx, N.ptr(mt_key), int(mt_state[2]), spp * 4 * npix, 4 * npix,
+                                                  jit_dev, N.ptr(mt_key_out), ctypes.byref(mt_pos_out)))
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
         if tile is not None:
             # rank tile -> torch buffer (device to device; srt_memcpy synchronises the library's

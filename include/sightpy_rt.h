@@ -240,6 +240,15 @@ int srt_intersect_collider(srt_ctx* ctx, const srt_collider* collider, const dou
                            const double* dir, int64_t n, double* out /* [2][n] */);
 int srt_primary_rays(srt_ctx* ctx, const srt_camera* cam, const double* jitter /* [4][n] */,
                      double* origin /* [3][n] */, double* dir /* [3][n] */);
+/* numpy's legacy global-RNG stream on the device: writes the n_out doubles that
+ * `np.random.rand(n_out)` would return for the RandomState with MT19937 key[624] and position
+ * pos (0..624, as in np.random.get_state()), then consumes n_skip more draws, and returns the
+ * resulting state (key_out, *pos_out) for np.random.set_state.  `out` may be device or host memory.
+ * Replaces the camera jitter draws of Camera.get_ray (sightpy/camera.py:56-64,
+ * utils/random.py:6-9) and the extra sizing draw of Scene.render (sightpy/scene.py:81), so that
+ * parity-mode renders need no host RNG and no host-to-device jitter copy. */
+int srt_mt19937_uniforms(srt_ctx* ctx, const uint32_t* key, int32_t pos, int64_t n_out, int64_t n_skip,
+                         double* out, uint32_t* key_out, int32_t* pos_out);
 /* Device memory helpers for callers that keep inputs resident in HBM (bench, multi-GPU). */
 int srt_device_alloc(srt_ctx* ctx, int64_t bytes, void** out);
 int srt_device_free(srt_ctx* ctx, void* ptr);

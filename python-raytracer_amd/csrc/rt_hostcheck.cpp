@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "rt_device.h"
+#include "rt_mt.h"
 
 using namespace rt;
 
@@ -249,6 +250,14 @@ int hc_primary_rays(const srt_camera* cam, const double* J, double* O, double* D
         O[i] = o.x; O[n + i] = o.y; O[2 * n + i] = o.z;
         D[i] = d.x; D[n + i] = d.y; D[2 * n + i] = d.z;
     }
+    return SRT_OK;
+}
+
+// numpy legacy rand stream by the segmented jump-ahead scheme of rt_mt.h, run serially
+int hc_mt_uniforms(const uint32_t* key, int pos, int64_t n_out, int64_t n_skip, double* out, uint32_t* key_out,
+                   int* pos_out) {
+    if (pos < 0 || pos > rtmt::N || n_out < 0 || n_skip < 0 || n_out + n_skip == 0) return SRT_ERR_ARG;
+    rtmt::uniforms_serial(key, pos, n_out, n_skip, out, key_out, pos_out);
     return SRT_OK;
 }
 

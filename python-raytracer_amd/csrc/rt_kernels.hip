@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "rt_device.h"
+#include "rt_mt.h"
 
 using namespace rt;
 
@@ -478,6 +479,122 @@ __global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, cons
     }
 }
 
+
+// ---- numpy legacy RNG stream on the device (rt_mt.h) ---------------------------------------------
+struct MtArgs {
+    const uint32_t* key;   // the round's key window (624 words)
+    const uint32_t* tab;   // jump tables: J1[16][624] then J2[15][624]
+    double* out;           // doubles of the whole call
+    uint32_t* chain_dst;   // next round's key window (written by segment SEGS-1) or null
+    uint32_t* dump_dst;    // final numpy key window or null
+    int64_t words;         // words consumed by this round
+    int64_t double_base;   // first double of this round
+    int64_t n_out;         // doubles to write (the rest are skipped draws)
+    int64_t dump_at;       // round-relative start of the final state window, or -1
+    int32_t pos;           // outputs start at word `pos` of the key window
+};
+
+constexpr int MT_THREADS = 256;
+
+// new block (624 words) of the raw sequence from the previous block, in three dependent phases
+__device__ __forceinline__ void mt_gen_block(const uint32_t* prev, uint32_t* next) {
+    const int t = threadIdx.x;
+    if (t < 227) next[t] = rtmt::next_word(prev[t], prev[t + 1], prev[t + 397]);
+    __syncthreads();
+    if (t < 227) next[227 + t] = rtmt::next_word(prev[227 + t], prev[228 + t], next[t]);
+    __syncthreads();
+    if (t < 170) {
+        const int i = 454 + t;
+        next[i] = rtmt::next_word(prev[i], i == 623 ? next[0] : prev[i + 1], next[i - 227]);
+    }
+    __syncthreads();
+}
+
+// win <- p(T) win : out[m] = XOR_{i : p_i} y[i + m] with y generated forward from win (rt_mt.h)
+__device__ void mt_jump(uint32_t* win, uint32_t* ring, const uint32_t* poly) {
+    const int t = threadIdx.x;
+    for (int m = t; m < rtmt::N; m += MT_THREADS) ring[m] = win[m];
+    __syncthreads();
+    mt_gen_block(ring, ring + rtmt::N);
+    uint32_t acc0 = 0u, acc1 = 0u, acc2 = 0u;
+    const int m0 = t, m1 = t + MT_THREADS, m2 = t + 2 * MT_THREADS;  // m2 < 624 for t < 112
+    for (int b = 0; b * rtmt::N < rtmt::POLY_BITS; ++b) {
+        // y[i + m] for i in block b lives in ring slots b & 1 and (b + 1) & 1: y[j] = ring[j % 1248]
+        const int i0 = b * rtmt::N, i1 = min(i0 + rtmt::N, rtmt::POLY_BITS);
+        for (int i = i0; i < i1;) {
+            const uint32_t w = __builtin_amdgcn_readfirstlane(poly[i >> 5]) >> (i & 31);
+            const int nb = min(32 - (i & 31), i1 - i);
+            for (int k = 0; k < nb; ++k) {
+                if ((w >> k) & 1u) {
+                    const int j = i + k;
+                    acc0 ^= ring[(j + m0) % (2 * rtmt::N)];
+                    acc1 ^= ring[(j + m1) % (2 * rtmt::N)];
+                    if (m2 < rtmt::N) acc2 ^= ring[(j + m2) % (2 * rtmt::N)];
+                }
+            }
+            i += nb;
+        }
+        __syncthreads();
+        // block b + 2 replaces block b (same slot), generated from block b + 1
+        mt_gen_block(ring + ((b + 1) & 1) * rtmt::N, ring + (b & 1) * rtmt::N);
+    }
+    win[m0] = acc0;
+    win[m1] = acc1;
+    if (m2 < rtmt::N) win[m2] = acc2;
+    __syncthreads();
+}
+
+// one workgroup per segment of the round: jump to the segment's window, generate its words,
+// write its doubles; the round's last segment hands the next round its key window, and the segment
+// holding the final state window copies it out
+__global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
+    __shared__ uint32_t win[rtmt::N];
+    __shared__ uint32_t ring[2 * rtmt::N];
+    const int s = blockIdx.x;
+    const int t = threadIdx.x;
+    for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
+    __syncthreads();
+    if (s > 0) {
+        const int b = ((s - 1) % 16) + 1, a = (s - b) / 16;
+        mt_jump(win, ring, A.tab + (int64_t)(b - 1) * rtmt::N);
+        if (a > 0) mt_jump(win, ring, A.tab + (int64_t)(16 + a - 1) * rtmt::N);
+    }
+    const int64_t ws = rtmt::window_start(s);
+    const int64_t end = A.pos + A.words;  // round-relative, exclusive
+    const int64_t lo = (int64_t)s * rtmt::L + A.pos;
+    const int64_t hi = min((int64_t)(s + 1) * rtmt::L + A.pos, end);
+    int64_t gen_end = hi;
+    const bool chain = A.chain_dst && s == rtmt::SEGS - 1;
+    const int64_t chain_at = rtmt::window_start(rtmt::SEGS);
+    if (chain) gen_end = max(gen_end, chain_at + rtmt::N);
+    const bool dump = A.dump_dst && rtmt::dumps(s, A.dump_at);
+    if (dump) gen_end = max(gen_end, A.dump_at + rtmt::N);
+    for (int m = t; m < rtmt::N; m += MT_THREADS) ring[m] = win[m];
+    __syncthreads();
+    for (int64_t q = 0; ws + q * rtmt::N < gen_end; ++q) {
+        if (q > 0) mt_gen_block(ring + ((q - 1) & 1) * rtmt::N, ring + (q & 1) * rtmt::N);
+        const int64_t b0 = ws + q * rtmt::N;  // absolute index of this block's first word
+        // pairs (a, a + 1) of the output whose second word is in this block
+        int64_t a0 = b0 - 1;
+        if (a0 < lo) a0 = lo;
+        if (((a0 - A.pos) & 1) != 0) ++a0;
+        for (int64_t a = a0 + 2 * t; a + 1 < b0 + rtmt::N && a < hi; a += 2 * MT_THREADS) {
+            const int64_t d = A.double_base + (a - A.pos) / 2;
+            if (d < A.n_out) {
+                const uint32_t w0 = ring[(a - ws) % (2 * rtmt::N)], w1 = ring[(a + 1 - ws) % (2 * rtmt::N)];
+                A.out[d] = rtmt::to_double(rtmt::temper(w0), rtmt::temper(w1));
+            }
+        }
+        for (int m = t; m < rtmt::N; m += MT_THREADS) {
+            const int64_t x = b0 + m;
+            const uint32_t v = ring[(q & 1) * rtmt::N + m];
+            if (chain && x >= chain_at && x < chain_at + rtmt::N) A.chain_dst[x - chain_at] = v;
+            if (dump && x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = v;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 struct srt_ctx {
@@ -517,6 +634,9 @@ struct srt_ctx {
     uint32_t* flags = nullptr;   // [2]
     unsigned long long* shadow = nullptr;
     std::vector<hipEvent_t> ev;
+    uint32_t* mt = nullptr;    // MT19937 jump tables (31 x 624) + two round keys + the final key
+    double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
+    int64_t mt_out_cap = 0;
     uint32_t* host = nullptr;  // pinned: per-pass counters/flags, shadow count
     int64_t host_words = 0;
 };
@@ -674,7 +794,8 @@ int srt_destroy(srt_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     free_list(c->scene_bufs);
     free_list(c->queue_bufs);
-    void* bufs[] = {c->fb, c->rgb, c->u8, c->xs, c->ys, c->rows, c->jit, c->hit, c->counts, c->flags, c->shadow};
+    void* bufs[] = {c->fb, c->rgb, c->u8, c->xs, c->ys, c->rows, c->jit, c->hit, c->counts, c->flags, c->shadow,
+                    c->mt, c->mt_out};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1137,6 +1258,56 @@ int srt_memcpy(srt_ctx* c, void* dst, const void* src, int64_t bytes) {
     if (!c || !dst || !src || bytes < 0) return fail(SRT_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault));
+    return SRT_OK;
+}
+
+int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n_out, int64_t n_skip, double* out,
+                         uint32_t* key_out, int32_t* pos_out) {
+    if (!c || !key || !key_out || !pos_out || (n_out > 0 && !out)) return fail(SRT_ERR_ARG, "null argument");
+    if (pos < 0 || pos > rtmt::N || n_out < 0 || n_skip < 0) return fail(SRT_ERR_ARG, "bad position or count");
+    if (is_device_ptr(key) || is_device_ptr(key_out)) return fail(SRT_ERR_ARG, "key and key_out are host arrays");
+    if (n_out + n_skip == 0) {
+        memcpy(key_out, key, rtmt::N * 4);
+        *pos_out = pos;
+        return SRT_OK;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    constexpr int64_t NTAB = 31 * rtmt::N;
+    if (!c->mt) {
+        HIP_TRY(dalloc(&c->mt, NTAB + 3 * rtmt::N));
+        HIP_TRY(hipMemcpyAsync(c->mt, rtmt::tables_flat(), NTAB * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    uint32_t* keys[2] = {c->mt + NTAB, c->mt + NTAB + rtmt::N};
+    uint32_t* dump = c->mt + NTAB + 2 * rtmt::N;
+    double* dst = out;
+    const bool host_out = n_out > 0 && !is_device_ptr(out);
+    if (host_out) {
+        int rc = ensure_buf(&c->mt_out, c->mt_out_cap, n_out);
+        if (rc) return rc;
+        dst = c->mt_out;
+    }
+    HIP_TRY(hipMemcpyAsync(keys[0], key, rtmt::N * 4, hipMemcpyHostToDevice, c->stream));
+    const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
+    for (size_t r = 0; r < plan.rounds.size(); ++r) {
+        const rtmt::Round& R = plan.rounds[r];
+        MtArgs A{};
+        A.key = keys[r & 1];
+        A.tab = c->mt;
+        A.out = dst;
+        A.chain_dst = R.chain ? keys[(r + 1) & 1] : nullptr;
+        A.dump_dst = R.dump_at >= 0 ? dump : nullptr;
+        A.words = R.words;
+        A.double_base = R.double_base;
+        A.n_out = n_out;
+        A.dump_at = R.dump_at;
+        A.pos = R.pos;
+        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), 0, c->stream, A);
+        HIP_TRY(hipGetLastError());
+    }
+    if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(key_out, dump, rtmt::N * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *pos_out = plan.final_pos;
     return SRT_OK;
 }
 

@@ -13,7 +13,7 @@ from . import _native as N
 from ._lower import lower_scene, camera_desc, collider_record
 from .utils.vector3 import vec3
 
-_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": None}
+_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": None, "buffers": {}}
 
 
 class RenderResult:
@@ -61,6 +61,41 @@ def upload(scene, extra_media=(), force=False):
     return L
 
 
+def device_buffer(name, nbytes):
+    """A named device allocation of the context, grown on demand (kept across calls)."""
+    lib, ctx = context()
+    cur = _STATE["buffers"].get(name)
+    if cur is not None and cur[1] >= nbytes:
+        return cur[0]
+    if cur is not None:
+        N.check(lib, lib.srt_device_free(ctx, cur[0]))
+        del _STATE["buffers"][name]
+    p = ctypes.c_void_p()
+    N.check(lib, lib.srt_device_alloc(ctx, max(int(nbytes), 8), ctypes.byref(p)))
+    _STATE["buffers"][name] = (p, int(nbytes))
+    return p
+
+
+def numpy_uniforms(n_out, n_skip=0, out=None):
+    """`np.random.rand(n_out)` computed on the GPU (then `n_skip` more draws), advancing numpy's
+    global RandomState exactly as the host draws would (srt_mt19937_uniforms).
+
+    Returns the doubles in a device buffer (a ctypes pointer, valid until the next call) when `out`
+    is None, else writes the host array `out`."""
+    lib, ctx = context()
+    name, key, pos, has_gauss, gauss = np.random.get_state()
+    if name != "MT19937":
+        raise ValueError("numpy's global generator is not MT19937")
+    key = np.ascontiguousarray(key, dtype=np.uint32)
+    dst = device_buffer("uniforms", 8 * n_out) if out is None else N.ptr(out)
+    key_out = np.empty(624, dtype=np.uint32)
+    pos_out = ctypes.c_int32(0)
+    N.check(lib, lib.srt_mt19937_uniforms(ctx, N.ptr(key), int(pos), int(n_out), int(n_skip), dst, N.ptr(key_out),
+                                          ctypes.byref(pos_out)))
+    np.random.set_state((name, key_out, pos_out.value, has_gauss, gauss))
+    return dst
+
+
 def _planar(v, n=None):
     """vec3 (scalars or arrays) -> C-contiguous float64 (3, n)."""
     comps = [np.asarray(c, dtype=np.float64) for c in (v.x, v.y, v.z)]
@@ -76,8 +111,10 @@ def _default_seed():
     return (int(key[pos % 624]) << 32 | int(key[(pos + 397) % 624])) ^ (int(pos) * 0x9E3779B97F4A7C15) & (2**64 - 1)
 
 
-def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False):
-    """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG."""
+def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False,
+                 jitter_device=None):
+    """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG;
+    `jitter_device`: the same uniforms already in device memory (numpy_uniforms)."""
     lib, ctx = context()
     upload(scene)
     cam = scene.camera
@@ -93,7 +130,9 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
     a.batch_spp = int(batch_size or 0)
     a.rows = N.ptr(rows_arr)
     j = None
-    if jitter is not None:
+    if jitter_device is not None:
+        a.jitter = jitter_device.value if isinstance(jitter_device, ctypes.c_void_p) else jitter_device
+    elif jitter is not None:
         j = np.ascontiguousarray(jitter, dtype=np.float64)
         if j.shape != (spp, 4, npix):
             raise ValueError("jitter must have shape (spp, 4, %d)" % npix)

@@ -196,6 +196,8 @@ SIGNATURES = {
     "srt_nearest": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, _p, _p]),
     "srt_intersect_collider": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int64, _p]),
     "srt_primary_rays": (ctypes.c_int, [_p, ctypes.POINTER(CameraDesc), _p, _p, _p]),
+    "srt_mt19937_uniforms": (ctypes.c_int, [_p, _p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _p, _p,
+                                            ctypes.POINTER(ctypes.c_int32)]),
     "srt_device_alloc": (ctypes.c_int, [_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
     "srt_device_free": (ctypes.c_int, [_p, _p]),
     "srt_memcpy": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64]),

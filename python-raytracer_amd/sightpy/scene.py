@@ -62,22 +62,28 @@ class Scene:
 
         rng="numpy" (default) draws the primary-ray jitter from numpy's global legacy RNG exactly
         as the reference does (including the extra sizing draw at scene.py:81), so seeded renders
-        match the reference.  rng="device" generates it on the GPU (Philox keyed by pixel and
-        sample).  `batch_size` bounds the samples traced per device pass (HBM budget).
+        match the reference: the stream is generated on the GPU (srt_mt19937_uniforms, bit-equal to
+        np.random.rand) and numpy's global state is advanced past it.  rng="numpy-host" draws the
+        same stream with numpy on the host.  rng="device" generates independent jitter on the GPU
+        (Philox keyed by pixel and sample).  `batch_size` bounds the samples per device pass.
         """
-        from ._backend import render_scene
+        from ._backend import render_scene, numpy_uniforms
 
         print("Rendering...")
         t0 = time.time()
-        jitter = None
-        if rng == "numpy":
+        world, rank = _dist_world()
+        jitter = jitter_dev = None
+        npix = int(self.camera.screen_width) * int(self.camera.screen_height)
+        if rng == "numpy" and world == 1:
+            jitter_dev = numpy_uniforms(samples_per_pixel * 4 * npix, 4 * npix)
+        elif rng in ("numpy", "numpy-host"):
             jitter = self.camera.draw_jitter(samples_per_pixel)
             self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
         elif rng != "device":
-            raise ValueError("rng must be 'numpy' or 'device'")
-        world, rank = _dist_world()
+            raise ValueError("rng must be 'numpy', 'numpy-host' or 'device'")
         if world == 1:
-            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size)
+            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size,
+                               jitter_device=jitter_dev)
             srgb8 = out.srgb8
         else:
             # one process per GPU under torch.distributed: render this rank's row bands, gather

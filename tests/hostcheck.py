@@ -29,6 +29,8 @@ def lib():
                                    [ctypes.c_void_p] * 3
         _lib.hc_intersect_collider.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_void_p]
         _lib.hc_primary_rays.argtypes = [ctypes.POINTER(N.CameraDesc)] + [ctypes.c_void_p] * 3
+        _lib.hc_mt_uniforms.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         _lib.hc_last_error.restype = ctypes.c_char_p
     return _lib
 
@@ -68,3 +70,15 @@ def intersect(collider, O, D):
     out = np.empty((2, O.shape[1]))
     lib().hc_intersect_collider(N.ptr(rec), N.ptr(O), N.ptr(D), O.shape[1], N.ptr(out))
     return out
+
+
+def mt_uniforms(key, pos, n_out, n_skip=0):
+    """rt_mt.h's segmented numpy-stream generator, run serially on the CPU."""
+    key = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.empty(n_out)
+    key_out = np.empty(624, dtype=np.uint32)
+    pos_out = ctypes.c_int(0)
+    rc = lib().hc_mt_uniforms(key.ctypes.data, int(pos), int(n_out), int(n_skip), out.ctypes.data,
+                              key_out.ctypes.data, ctypes.byref(pos_out))
+    assert rc == 0, rc
+    return out, key_out, pos_out.value

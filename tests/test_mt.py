@@ -1,0 +1,117 @@
+"""numpy's legacy `np.random.rand` stream reproduced by the segmented MT19937 jump-ahead scheme
+(python-raytracer_amd/csrc/rt_mt.h, tables from tools/gen_mt_jump.py).  The oracle is numpy itself
+(the stream the reference draws its camera jitter from: camera.py:51-85, utils/random.py:6-9); the
+CPU tests run the scheme serially through the host-check build, the GPU tests run the HIP kernel
+through the C ABI.  Bar: bit-exact doubles and an identical final numpy state."""
+import sys
+
+import numpy as np
+import pytest
+
+import hostcheck as HC
+from conftest import ROOT
+
+L_DOUBLES = (1 << 19) // 2  # doubles per device segment
+
+
+def numpy_case(seed, pre, n_out, n_skip):
+    rs = np.random.RandomState(seed)
+    rs.random_sample(pre)
+    st = rs.get_state()
+    want = rs.random_sample(n_out)
+    rs.random_sample(n_skip)
+    end = rs.get_state()
+    return st, want, end
+
+
+CASES = [
+    # seed, doubles drawn before (sets pos), n_out, n_skip
+    (0, 0, 1000, 0),             # fresh seed: pos = 624
+    (1, 1, 4097, 3),             # odd position
+    (2, 311, 10, 0),             # pos = 622: first pair straddles a regeneration
+    (3, 312, 1, 0),              # pos = 624 after draws
+    (4, 5, 2 * L_DOUBLES + 17, 100),   # three segments (jumps x^(L-1), x^(2L-1))
+    (5, 100, L_DOUBLES - 1, 2),  # ends right at a segment boundary
+    (6, 7, 100, 17 * L_DOUBLES),  # skipped draws cross 17 segments (second-level jump)
+    (7, 3, 256 * L_DOUBLES + 1000, 5),  # outputs cross a round (256 segments): chained key window
+    (8, 620, 40, 256 * L_DOUBLES - 45),  # final state window lands in the previous round
+]
+
+
+@pytest.mark.parametrize("seed,pre,n_out,n_skip", CASES)
+def test_mt_segments_match_numpy_cpu(seed, pre, n_out, n_skip):
+    st, want, end = numpy_case(seed, pre, n_out, n_skip)
+    got, key, pos = HC.mt_uniforms(st[1], st[2], n_out, n_skip)
+    assert np.array_equal(got, want)
+    assert pos == end[2] and np.array_equal(key, end[1])
+
+
+def test_jump_table_is_the_mt19937_jump():
+    """Re-derive two table entries independently (pure Python MT words) and compare."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import gen_mt_jump as G
+
+    src = (ROOT / "python-raytracer_amd" / "csrc" / "rt_mt_jump.h").read_text()
+    import re
+
+    def table(name):
+        body = src.split("static const uint32_t %s" % name)[1].split("};")[0]
+        return [sum(int(v, 16) << (32 * k) for k, v in enumerate(r.split(",")))
+                for r in re.findall(r"\{(0x[^{}]*)\}", body)]
+
+    j1 = table("RT_MT_J1")
+    assert len(j1) == 16 and len(table("RT_MT_J2")) == 15
+    G.check_jump(j1[0], G.L - 1)
+
+
+def _device_uniforms(st, n_out, n_skip, device_out=False):
+    import ctypes
+    from sightpy import _backend as B, _native as N
+
+    np.random.set_state(st)
+    if device_out:
+        lib, ctx = B.context()
+        p = B.numpy_uniforms(n_out, n_skip)
+        got = np.empty(n_out)
+        N.check(lib, lib.srt_memcpy(ctx, N.ptr(got), p, 8 * n_out))
+    else:
+        got = np.empty(n_out)
+        B.numpy_uniforms(n_out, n_skip, out=got)
+    return got, np.random.get_state()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,pre,n_out,n_skip", CASES)
+def test_mt_device_matches_numpy(seed, pre, n_out, n_skip):
+    st, want, end = numpy_case(seed, pre, n_out, n_skip)
+    got, after = _device_uniforms(st, n_out, n_skip)
+    assert np.array_equal(got, want)
+    assert after[2] == end[2] and np.array_equal(after[1], end[1])
+
+
+@pytest.mark.gpu
+def test_mt_device_1080p_jitter_stream():
+    """The parity-mode draw of Scene.render at the headline config (6 spp + the sizing draw at
+    1920x1080), generated into device memory, equals numpy's stream."""
+    npix = 1920 * 1080
+    st, want, end = numpy_case(0, 0, 6 * 4 * npix, 4 * npix)
+    got, after = _device_uniforms(st, 6 * 4 * npix, 4 * npix, device_out=True)
+    assert np.array_equal(got, want)
+    assert after[2] == end[2] and np.array_equal(after[1], end[1])
+
+
+@pytest.mark.gpu
+def test_scene_render_device_stream_equals_host_stream():
+    import scenes
+
+    sc = scenes.example1(160, 120, 3)
+    np.random.seed(5)
+    a = np.asarray(sc.render(2, rng="numpy"))
+    sa = np.random.get_state()
+    np.random.seed(5)
+    b = np.asarray(sc.render(2, rng="numpy-host"))
+    sb = np.random.get_state()
+    # same jitter; the framebuffer's depth >= 1 atomics may round a u8 differently
+    d = np.abs(a.astype(int) - b.astype(int))
+    assert d.max() <= 1 and (d > 0).mean() < 1e-3
+    assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
