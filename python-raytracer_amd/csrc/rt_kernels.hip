@@ -494,54 +494,93 @@ struct MtArgs {
     int32_t pos;           // outputs start at word `pos` of the key window
 };
 
-constexpr int MT_THREADS = 256;
+constexpr int MT_THREADS = 320;  // 5 waves: one output pair per thread per 624-word block
+// LDS ring of 624-word blocks: block q in slot q % 3, slot 3 mirrors slot 0 so that any two
+// consecutive blocks are contiguous (slots s, s + 1)
+constexpr int MT_SLOTS = 4;
 
-// new block (624 words) of the raw sequence from the previous block, in three dependent phases
-__device__ __forceinline__ void mt_gen_block(const uint32_t* prev, uint32_t* next) {
-    const int t = threadIdx.x;
-    if (t < 227) next[t] = rtmt::next_word(prev[t], prev[t + 1], prev[t + 397]);
-    __syncthreads();
-    if (t < 227) next[227 + t] = rtmt::next_word(prev[227 + t], prev[228 + t], next[t]);
-    __syncthreads();
-    if (t < 170) {
-        const int i = 454 + t;
-        next[i] = rtmt::next_word(prev[i], i == 623 ? next[0] : prev[i + 1], next[i - 227]);
-    }
-    __syncthreads();
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic, not for its global
+// stores (__syncthreads() would also drain the output stores every block)
+__device__ __forceinline__ void mt_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+    __builtin_amdgcn_s_barrier();
 }
 
-// win <- p(T) win : out[m] = XOR_{i : p_i} y[i + m] with y generated forward from win (rt_mt.h)
-__device__ void mt_jump(uint32_t* win, uint32_t* ring, const uint32_t* poly) {
+__device__ __forceinline__ void mt_store(uint32_t* ring, int slot, int i, uint32_t v) {
+    ring[slot * rtmt::N + i] = v;
+    if (slot == 0) ring[3 * rtmt::N + i] = v;
+}
+
+// block q+1 from block q (slot `ps`) into slot `ns`.  Thread t < 227 makes words t, 227 + t and
+// 454 + t: each needs only the previous block and the thread's own earlier word (x_{k+624} =
+// x_{k+397} ^ twist(x_k, x_{k+1}); k + 397 - 624 is t, then 227 + t), so no barrier is needed
+// inside the block; word 623 also needs word 0, which thread 169 recomputes.
+__device__ __forceinline__ void mt_gen_block(uint32_t* ring, int ps, int ns) {
     const int t = threadIdx.x;
-    for (int m = t; m < rtmt::N; m += MT_THREADS) ring[m] = win[m];
+    if (t < 227) {
+        const uint32_t* p = ring + ps * rtmt::N;
+        const uint32_t wa = rtmt::next_word(p[t], p[t + 1], p[t + 397]);
+        const uint32_t wb = rtmt::next_word(p[227 + t], p[228 + t], wa);
+        mt_store(ring, ns, t, wa);
+        mt_store(ring, ns, 227 + t, wb);
+        if (t < 170) {
+            const uint32_t x1 = (t == 169) ? rtmt::next_word(p[0], p[1], p[397]) : p[455 + t];
+            mt_store(ring, ns, 454 + t, rtmt::next_word(p[454 + t], x1, wb));
+        }
+    }
+}
+
+// win <- p(T) win : out[m] = XOR_{i : p_i} y[i + m] with y generated forward from win (rt_mt.h).
+// Thread t owns m = t and t + MT_THREADS.  Set coefficient bits are taken four at a time with
+// scalar find-first-set and their eight LDS reads issued together (predicated when fewer remain).
+__device__ void mt_jump(uint32_t* win, uint32_t* ring, uint32_t* coef, const uint32_t* poly) {
+    const int t = threadIdx.x;
+    for (int m = t; m < rtmt::N; m += MT_THREADS) {
+        mt_store(ring, 0, m, win[m]);
+        coef[m] = poly[m];  // the 19937 coefficient bits, staged once (624 words)
+    }
     __syncthreads();
-    mt_gen_block(ring, ring + rtmt::N);
-    uint32_t acc0 = 0u, acc1 = 0u, acc2 = 0u;
-    const int m0 = t, m1 = t + MT_THREADS, m2 = t + 2 * MT_THREADS;  // m2 < 624 for t < 112
+    mt_gen_block(ring, 0, 1);
+    mt_barrier();
+    const int m0 = t, m1 = t + MT_THREADS;  // m1 < 624 for t < 304
+    const int m1c = m1 < rtmt::N ? m1 : 0;
+    uint32_t acc0 = 0u, acc1 = 0u;
     for (int b = 0; b * rtmt::N < rtmt::POLY_BITS; ++b) {
-        // y[i + m] for i in block b lives in ring slots b & 1 and (b + 1) & 1: y[j] = ring[j % 1248]
+        mt_gen_block(ring, (b + 1) % 3, (b + 2) % 3);  // block b + 2 (overwrites block b - 1)
+        const uint32_t* yb = ring + (b % 3) * rtmt::N;  // y[624 b + x], x < 1248
         const int i0 = b * rtmt::N, i1 = min(i0 + rtmt::N, rtmt::POLY_BITS);
-        for (int i = i0; i < i1;) {
-            const uint32_t w = __builtin_amdgcn_readfirstlane(poly[i >> 5]) >> (i & 31);
-            const int nb = min(32 - (i & 31), i1 - i);
-            for (int k = 0; k < nb; ++k) {
-                if ((w >> k) & 1u) {
-                    const int j = i + k;
-                    acc0 ^= ring[(j + m0) % (2 * rtmt::N)];
-                    acc1 ^= ring[(j + m1) % (2 * rtmt::N)];
-                    if (m2 < rtmt::N) acc2 ^= ring[(j + m2) % (2 * rtmt::N)];
+        for (int wi = i0 >> 5; wi <= (i1 - 1) >> 5; ++wi) {
+            uint32_t w = __builtin_amdgcn_readfirstlane(coef[wi]);
+            const int lo = max(i0 - wi * 32, 0), hi = min(i1 - wi * 32, 32);
+            w &= (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+            const uint32_t* yw = yb + (wi * 32 - i0);
+            while (w) {
+                int k[4];
+                uint32_t keep[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    keep[u] = w ? 0xFFFFFFFFu : 0u;
+                    k[u] = w ? __builtin_ctz(w) : 0;
+                    w &= w - 1u;
+                }
+                uint32_t r0[4], r1[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    r0[u] = yw[k[u] + m0];
+                    r1[u] = yw[k[u] + m1c];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc0 ^= r0[u] & keep[u];
+                    acc1 ^= r1[u] & keep[u];
                 }
             }
-            i += nb;
         }
-        __syncthreads();
-        // block b + 2 replaces block b (same slot), generated from block b + 1
-        mt_gen_block(ring + ((b + 1) & 1) * rtmt::N, ring + (b & 1) * rtmt::N);
+        mt_barrier();
     }
     win[m0] = acc0;
-    win[m1] = acc1;
-    if (m2 < rtmt::N) win[m2] = acc2;
-    __syncthreads();
+    if (m1 < rtmt::N) win[m1] = acc1;
+    mt_barrier();
 }
 
 // one workgroup per segment of the round: jump to the segment's window, generate its words,
@@ -549,15 +588,16 @@ __device__ void mt_jump(uint32_t* win, uint32_t* ring, const uint32_t* poly) {
 // holding the final state window copies it out
 __global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
     __shared__ uint32_t win[rtmt::N];
-    __shared__ uint32_t ring[2 * rtmt::N];
+    __shared__ uint32_t ring[MT_SLOTS * rtmt::N];
+    __shared__ uint32_t coef[rtmt::N];
     const int s = blockIdx.x;
     const int t = threadIdx.x;
     for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
     __syncthreads();
     if (s > 0) {
         const int b = ((s - 1) % 16) + 1, a = (s - b) / 16;
-        mt_jump(win, ring, A.tab + (int64_t)(b - 1) * rtmt::N);
-        if (a > 0) mt_jump(win, ring, A.tab + (int64_t)(16 + a - 1) * rtmt::N);
+        mt_jump(win, ring, coef, A.tab + (int64_t)(b - 1) * rtmt::N);
+        if (a > 0) mt_jump(win, ring, coef, A.tab + (int64_t)(16 + a - 1) * rtmt::N);
     }
     const int64_t ws = rtmt::window_start(s);
     const int64_t end = A.pos + A.words;  // round-relative, exclusive
@@ -569,29 +609,36 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
     if (chain) gen_end = max(gen_end, chain_at + rtmt::N);
     const bool dump = A.dump_dst && rtmt::dumps(s, A.dump_at);
     if (dump) gen_end = max(gen_end, A.dump_at + rtmt::N);
-    for (int m = t; m < rtmt::N; m += MT_THREADS) ring[m] = win[m];
+    for (int m = t; m < rtmt::N; m += MT_THREADS) mt_store(ring, 0, m, win[m]);
     __syncthreads();
+    // output pairs are (pos + 2k, pos + 2k + 1); a block emits the pairs whose second word it holds
+    int64_t a_first = lo;
+    if (((a_first - A.pos) & 1) != 0) ++a_first;
     for (int64_t q = 0; ws + q * rtmt::N < gen_end; ++q) {
-        if (q > 0) mt_gen_block(ring + ((q - 1) & 1) * rtmt::N, ring + (q & 1) * rtmt::N);
+        const int slot = (int)(q % 3);
         const int64_t b0 = ws + q * rtmt::N;  // absolute index of this block's first word
-        // pairs (a, a + 1) of the output whose second word is in this block
-        int64_t a0 = b0 - 1;
-        if (a0 < lo) a0 = lo;
+        if (ws + (q + 1) * rtmt::N < gen_end) mt_gen_block(ring, slot, (slot + 1) % 3);
+        int64_t a0 = b0 - 1 > a_first ? b0 - 1 : a_first;
         if (((a0 - A.pos) & 1) != 0) ++a0;
-        for (int64_t a = a0 + 2 * t; a + 1 < b0 + rtmt::N && a < hi; a += 2 * MT_THREADS) {
+        const int64_t a = a0 + 2 * t;
+        if (a + 1 < b0 + rtmt::N && a < hi) {
             const int64_t d = A.double_base + (a - A.pos) / 2;
             if (d < A.n_out) {
-                const uint32_t w0 = ring[(a - ws) % (2 * rtmt::N)], w1 = ring[(a + 1 - ws) % (2 * rtmt::N)];
+                const int off = (int)(a - b0);  // -1: last word of the previous block
+                const uint32_t w0 = off >= 0 ? ring[slot * rtmt::N + off] : ring[((slot + 2) % 3) * rtmt::N + 623];
+                const uint32_t w1 = ring[slot * rtmt::N + off + 1];
                 A.out[d] = rtmt::to_double(rtmt::temper(w0), rtmt::temper(w1));
             }
         }
-        for (int m = t; m < rtmt::N; m += MT_THREADS) {
-            const int64_t x = b0 + m;
-            const uint32_t v = ring[(q & 1) * rtmt::N + m];
-            if (chain && x >= chain_at && x < chain_at + rtmt::N) A.chain_dst[x - chain_at] = v;
-            if (dump && x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = v;
+        if (chain || dump) {
+            for (int m = t; m < rtmt::N; m += MT_THREADS) {
+                const int64_t x = b0 + m;
+                const uint32_t v = ring[slot * rtmt::N + m];
+                if (chain && x >= chain_at && x < chain_at + rtmt::N) A.chain_dst[x - chain_at] = v;
+                if (dump && x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = v;
+            }
         }
-        __syncthreads();
+        mt_barrier();
     }
 }
 
