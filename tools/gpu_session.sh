@@ -20,7 +20,7 @@ run() {
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 900 python3 -m pytest tests/test_gpu.py -q -m gpu --timeout=300 -rf ;;
+    tests) run tests 900 python3 -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
