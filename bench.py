@@ -106,6 +106,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--occupancy", type=int, default=0, help="experiment: kernel variant with this waves/SIMD bound")
+    ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job, to size the per-rank work "
+                         "of the multi-GPU run without the gather")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,12 +131,16 @@ def main():
     builder, W, H, depth, spp, label = CONFIGS[args.config]
     if args.spp:
         spp = args.spp
+    if args.size:
+        W, H = (int(v) for v in args.size.lower().split("x"))
     sc = getattr(scenes, builder)(W, H, depth)
     lib, ctx = B.context()
     if args.occupancy:
         N.check(lib, lib.srt_set_option(ctx, b"occupancy", args.occupancy))
     B.upload(sc)
     rows = shard_rows(H, world, rank) if world > 1 else np.arange(H)
+    if args.shard_of > 1 and world == 1:
+        rows = shard_rows(H, args.shard_of, 0)
     npix = len(rows) * W
     # resident inputs: jitter (reference stream, seed 0) in HBM
     jit_dev = None
@@ -246,7 +254,8 @@ def main():
             "data": "synthetic: %s; jitter = reference numpy stream seed 0 (%s)" % (label, args.rng),
             "config": {"workload": label, "width": W, "height": H, "max_ray_depth": depth, "spp": spp,
                        "rays_per_frame": int(total_rays), "rays_per_depth_rank0": rpd,
-                       "shadow_rays_rank0": stats[0]["shadow_rays"], "parallelism": "row-band shards x%d" % world,
+                       "shadow_rays_rank0": stats[0]["shadow_rays"], "parallelism": ("row-band shards x%d" % world) if not args.shard_of
+                       else "diagnostic: rank 0 of %d row-band shards, no gather" % args.shard_of,
                        "frame_ms": round(ms_step, 4)},
             "roofline": {"bound": "hbm", "kernel": "k_primary (depth 0: raygen + nearest hit + shading, fused)",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -67,6 +67,38 @@ RT_HD d3 divs(d3 a, double s) { return d3{a.x / s, a.y / s, a.z / s}; }
 RT_HD double dot(d3 a, d3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 RT_HD bool is_zero(d3 a) { return a.x == 0.0 && a.y == 0.0 && a.z == 0.0; }
 
+// Several quotients a_i / b with one divisor.  On the GPU a float64 division is an 11-instruction
+// sequence (div_scale x2, rcp, two Newton steps, q = a*y, r = fma(-b, q, a), div_fmas, div_fixup);
+// for operands in the normal range div_scale/div_fmas/div_fixup change nothing, so the refined
+// reciprocal y can be computed once and each further quotient costs q = a*y, r = fma(-b, q, a),
+// q' = fma(r, y, q) -- the same instructions, hence bit-identical (correctly rounded, as numpy).
+// Divisors outside [1e-100, 1e100] (or NaN/inf/0) take the plain division.  Numerators must be
+// finite and below 1e100 in magnitude (true at every call site: geometry within FARAWAY = 1e39).
+struct Quot {
+    double b, y;
+    bool fast;
+    RT_HDM explicit Quot(double den) : b(den), y(0.0), fast(false) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const double ab = fabs(den);
+        fast = ab > 1e-100 && ab < 1e100;
+        if (fast) {
+            double r = __builtin_amdgcn_rcp(den);
+            r = fma(r, fma(-den, r, 1.0), r);
+            y = fma(r, fma(-den, r, 1.0), r);
+        }
+#endif
+    }
+    RT_HDM double operator()(double a) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (fast) {
+            const double q = a * y;
+            return fma(fma(-b, q, a), y, q);
+        }
+#endif
+        return a / b;
+    }
+};
+
 // vec3.normalize (vector3.py:158-160): v * (1.0 / where(|v| == 0, 1, |v|))
 RT_HD d3 normalize(d3 v) {
     double mag = sqrt(dot(v, v));
@@ -184,6 +216,8 @@ RT_HD double sphere_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     double b = 2.0 * dot(D, sub(O, C));
     double c = ((p[5] + dot(O, O)) - 2.0 * dot(C, O)) - p[6];
     double disc = b * b - 4.0 * c;
+    // disc <= 0 (or NaN) misses whatever h is (ok below needs disc > 0): skip the rest
+    if (!(disc > 0.0)) { o = FARAWAY; return FARAWAY; }
     double sq = sqrt(np_max(0.0, disc));
     double h0 = (-b - sq) / 2.0;
     double h1 = (-b + sq) / 2.0;
@@ -203,7 +237,10 @@ RT_HD double plane_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     double nd = dot(N, D);
     nd = (nd == 0.0) ? nd + 0.0001 : nd;
     double nco = dot(N, sub(ld3(p), O));
-    d3 d = d3{(D.x * nco) / nd, (D.y * nco) / nd, (D.z * nco) / nd};
+    // the hit needs nco * nd > 0 (same product as below; NaN fails too): skip the rest otherwise
+    if (!(nco * nd > 0.0)) { o = FARAWAY; return FARAWAY; }
+    const Quot q(nd);
+    d3 d = d3{q(D.x * nco), q(D.y * nco), q(D.z * nco)};
     d3 M = add(O, d);
     double dis = sqrt(dot(d, d));
     d3 MC = sub(M, ld3(p));
@@ -246,7 +283,9 @@ RT_HD double triangle_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     double nd = dot(N, D);
     nd = (nd == 0.0) ? nd + 0.0001 : nd;
     double nco = dot(N, sub(ld3(p), O));
-    d3 d = d3{(D.x * nco) / nd, (D.y * nco) / nd, (D.z * nco) / nd};
+    if (!(nco * nd > 0.0)) { o = FARAWAY; return FARAWAY; }  // as plane_hit
+    const Quot q(nd);
+    d3 d = d3{q(D.x * nco), q(D.y * nco), q(D.z * nco)};
     d3 M = add(O, d);
     double dis = sqrt(dot(d, d));
     bool inside = dot(ld3(p + 15), sub(M, ld3(p + 6))) >= 0.0 &&
@@ -448,9 +487,15 @@ struct Ray {
 RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double j[4], d3& O, d3& D) {
     double x = xc + ((j[0] - 0.5) * cam.cam_width) / (double)cam.width;
     double y = yr + ((j[1] - 0.5) * cam.cam_height) / (double)cam.height;
-    double r = sqrt(j[2]);
-    double phi = (j[3] * 2.0) * PI;
-    double rx = r * cos(phi), ry = r * sin(phi);
+    // pinhole (lens_radius == 0, every example): the disk offsets are (r cos, r sin) * 0 = +-0 and
+    // leave O = look_from, so the sqrt/sincos of the disk sample are skipped (0 stands in for them)
+    double rx = 0.0, ry = 0.0;
+    if (cam.lens_radius != 0.0) {
+        double r = sqrt(j[2]);
+        double phi = (j[3] * 2.0) * PI;
+        rx = r * cos(phi);
+        ry = r * sin(phi);
+    }
     d3 lf = ld3(cam.look_from), R = ld3(cam.right), U = ld3(cam.up);
     O = add(add(lf, mul(mul(R, rx), cam.lens_radius)), mul(mul(U, ry), cam.lens_radius));
     d3 t = add(add(add(lf, mul(mul(U, y), cam.focal_distance)), mul(mul(R, x), cam.focal_distance)),
@@ -469,7 +514,18 @@ RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bo
     bool nan = false;
     for (int c = 0; c < S.ncol; ++c) {
         double o;
-        double t = collider_hit(S.col[c], O, D, o);
+        const RT_RO srt_collider& cc = S.col[c];
+        if (cc.type == SRT_CUBOID && cc.p[42] != 0.0 && id >= 0) {
+            // axis-aligned box around O (a SkyBox): leaving it takes t >= dmin / max|D_i|, dmin the
+            // distance from O to the nearest face, and its slab t's are NaN-free (no face passes
+            // through O).  Far beyond the nearest hit so far it can be neither nearest nor tied.
+            const RT_RO double* p = cc.p;
+            double dmin = np_min(np_min(np_min(O.x - p[12], p[15] - O.x), np_min(O.y - p[13], p[16] - O.y)),
+                                 np_min(O.z - p[14], p[17] - O.z));
+            double dmax = np_max(np_max(fabs(D.x), fabs(D.y)), fabs(D.z));
+            if (dmin > 0.0 && best * dmax < 0.5 * dmin) continue;
+        }
+        double t = collider_hit(cc, O, D, o);
         if (t != t) nan = true;
         if (t < best) { best = t; id = c; bo = o; ties = false; }
         else if (t == best && id >= 0) ties = true;
@@ -603,7 +659,9 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
             double Dphong = (pow(np_clip(dot(N, H), 0.0, 1.0), m.p[4]) * m.p[5]) / m.p[6];
 #endif
             double den = 4.0 * np_clip(dot(N, V) * NdotL, 0.001, 1.0);
-            d3 spec = mul(mul(mul(divs(mul(F, Dphong), den), seelight), lv), m.p[7]);
+            const Quot qd(den);
+            d3 FD = mul(F, Dphong);
+            d3 spec = mul(mul(mul(d3{qd(FD.x), qd(FD.y), qd(FD.z)}, seelight), lv), m.p[7]);
             color = add(color, spec);
         }
     }

@@ -32,6 +32,11 @@ for step in "$@"; do
     pmc_list) run pmc_list 120 rocprofv3 -L ;;
     pmc_sq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_sq1 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
             run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    shard8) run bench_shard8 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 8
+            run bench_shard4 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 4
+            run bench_shard2 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 2 ;;
+    latency) run prof_latency 300 rocprofv3 --kernel-trace -d gpurun_out/prof_latency -o lat --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --size 64x1 --spp 1
+             run prof_shard8 300 rocprofv3 --kernel-trace -d gpurun_out/prof_shard8 -o s8 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --shard-of 8 ;;
     rngdev) run bench_rngdev 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --rng device ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
