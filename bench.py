@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--occupancy", type=int, default=0, help="experiment: kernel variant with this waves/SIMD bound")
+    ap.add_argument("--sync", action="store_true",
+                    help="one frame at a time (host waits for each frame) instead of pipelined frames")
     ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job, to size the per-rank work "
@@ -115,18 +117,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ.setdefault("SIGHTPY_DEVICE", str(local))
+    # rehearsal of the N-rank path on a box with fewer GPUs (never used by the driver):
+    # SIGHTPY_BENCH_DEVICE=k puts every rank on GPU k, SIGHTPY_BENCH_BACKEND=gloo gathers on the host
+    dev = int(os.environ.get("SIGHTPY_BENCH_DEVICE", local))
+    backend = os.environ.get("SIGHTPY_BENCH_BACKEND", "nccl")
+    os.environ.setdefault("SIGHTPY_DEVICE", str(dev))
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(dev)
+        dist.init_process_group(backend)
 
     import scenes
     from sightpy import _backend as B, _native as N
-    from sightpy._shard import shard_rows, gather_rows
+    from sightpy._shard import shard_rows, max_shard_rows, RowGather
 
     builder, W, H, depth, spp, label = CONFIGS[args.config]
     if args.spp:
@@ -177,28 +183,54 @@ def main():
     a.seed = 12345
     a.out_rgb, a.out_srgb8, a.out_hit_id = out_rgb, out_u8, None
 
-    tile = None
+    # Frames are pipelined: each step queues its frame on the library's stream (SRT_RENDER_ASYNC)
+    # and returns, so the host prepares frame k+1 while the GPU renders frame k; srt_render_finish
+    # at the end checks every frame's error flags.  With N ranks the frame's uint8 tile (written in
+    # place by k_resolve, double-buffered) is all-gathered over RCCL on torch's stream after the
+    # frame, overlapping the next frame's rendering.
+    pipelined = not args.sync and args.rng != "mt"
+    tiles, done = None, [None, None]
     if dist is not None:
         import torch
 
-        tile = torch.zeros((len(rows), W, 3), dtype=torch.uint8, device="cuda")
-    frame = {}
+        # each rank's uint8 tile, padded to the largest shard: the send buffer of the all-gather
+        tiles = [torch.zeros((max_shard_rows(H, world), W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        gather = RowGather(H, world, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
+        sp = ctypes.c_void_p()
+        N.check(lib, lib.srt_stream(ctx, ctypes.byref(sp)))
+        lib_stream = torch.cuda.ExternalStream(sp.value, device=torch.device("cuda", dev))
+    frame = {"k": 0}
 
-    def step(st):
+    def step(st, async_ok=True):
         if args.rng == "mt":
             # the reference's stream (seed 0): spp x 4 x npix jitter + the sizing draw, on the GPU
             N.check(lib, lib.srt_mt19937_uniforms(ctx, N.ptr(mt_key), int(mt_state[2]), spp * 4 * npix, 4 * npix,
                                                   jit_dev, N.ptr(mt_key_out), ctypes.byref(mt_pos_out)))
+        i = frame["k"] % 2
+        frame["k"] += 1
+        if tiles is not None:
+            if done[i] is not None:
+                lib_stream.wait_event(done[i])  # the gather that read this tile two frames ago
+            a.out_srgb8 = ctypes.c_void_p(tiles[i].data_ptr())
+        a.flags = N.RENDER_ASYNC if (pipelined and async_ok) else 0
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
-        if tile is not None:
-            # rank tile -> torch buffer (device to device; srt_memcpy synchronises the library's
-            # stream), then one RCCL all-gather over xGMI and the row un-permutation on device
-            N.check(lib, lib.srt_memcpy(ctx, ctypes.c_void_p(tile.data_ptr()), out_u8, 3 * npix))
-            frame["image"] = gather_rows(tile, H, world)
+        if tiles is not None:
+            import torch
+
+            cur = torch.cuda.current_stream()
+            cur.wait_stream(lib_stream)  # this frame's tile is complete
+            if backend == "nccl":
+                frame["image"] = gather(tiles[i])
+            else:
+                cur.synchronize()
+                frame["image"] = gather(tiles[i].cpu())
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            done[i] = ev
 
     st = N.Stats()
-    for _ in range(args.warmup):
-        step(st)
+    for w in range(args.warmup):
+        step(st, async_ok=w > 0)  # the first frame runs synchronously (sizes the queues)
 
     def barrier():
         if dist is not None:
@@ -207,22 +239,29 @@ def main():
             torch.cuda.synchronize()
         N.check(lib, lib.srt_synchronize(ctx))
 
-    stats = []
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        s = N.Stats()
-        step(s)
-        stats.append(s.as_dict())
+        step(st)
     barrier()
     elapsed = time.perf_counter() - t0
+    N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(st)))  # error flags of every pipelined frame
+    # kernel durations (HIP events on the library's stream) of the same frame, rendered one at a
+    # time so that every frame's events can be read: the roofline's per-launch times
+    stats = []
+    for _ in range(max(1, min(args.steps, 10))):
+        s = N.Stats()
+        step(s, async_ok=False)
+        stats.append(s.as_dict())
+    barrier()
     if dist is not None:
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        cdev = "cuda" if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        rays_local = torch.tensor([stats[0]["total_rays"]], dtype=torch.float64, device="cuda")
+        rays_local = torch.tensor([stats[0]["total_rays"]], dtype=torch.float64, device=cdev)
         dist.all_reduce(rays_local)
         total_rays = float(rays_local.item())
     else:

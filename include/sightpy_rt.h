@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 1
+#define SRT_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------------------------ */
 #define SRT_OK 0
@@ -196,7 +196,17 @@ typedef struct srt_render_args {
     double* out_rgb;      /* [3][n_rows*width] linear RGB averaged over spp, or NULL */
     uint8_t* out_srgb8;   /* [n_rows*width][3] resolved image, or NULL */
     int32_t* out_hit_id;  /* [spp][n_rows*width] primary nearest collider (-1 miss), or NULL */
+    int32_t flags;        /* SRT_RENDER_* */
+    int32_t reserved;
 } srt_render_args;
+
+/* SRT_RENDER_ASYNC: queue the frame on the context's stream and return at once (jitter and outputs
+ * must be device memory or NULL; `stats` is not written).  Consecutive asynchronous frames of the
+ * same shape pipeline back to back without host round trips; srt_render_finish waits for them,
+ * checks their error flags and returns the last one's stats.  Any other call on the context first
+ * finishes pending frames.  (No reference counterpart: Scene.render is synchronous; this serves
+ * frame sequences such as create_animation and the multi-GPU frame loop.) */
+#define SRT_RENDER_ASYNC 1
 
 #define SRT_MAX_DEPTHS 64
 typedef struct srt_stats {
@@ -229,10 +239,15 @@ int srt_abi_version(void);
 int srt_device_count(int* count);
 int srt_create(int device, srt_ctx** out);
 int srt_destroy(srt_ctx* ctx);
-/* options: "queue_bytes" (HBM budget for ray queues), "block_size" (reserved) */
+/* options: "queue_bytes" (HBM budget for ray queues), "max_blocks" (grid cap of the wavefront
+ * kernels), "frame_kernel" (-1 auto = frame kernel for branching scenes, 0 per-depth wavefront
+ * kernels, 1 frame kernel), "occupancy" (experiment: waves/SIMD bound of the ex1 variant) */
 int srt_set_option(srt_ctx* ctx, const char* key, int64_t value);
 int srt_upload_scene(srt_ctx* ctx, const srt_scene_desc* scene);
 int srt_render(srt_ctx* ctx, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);
+int srt_render_finish(srt_ctx* ctx, srt_stats* stats);
+/* the hipStream_t every call on ctx is ordered on (for stream/event interop, e.g. torch) */
+int srt_stream(srt_ctx* ctx, void** stream);
 int srt_trace(srt_ctx* ctx, const srt_trace_args* args, srt_stats* stats);
 int srt_nearest(srt_ctx* ctx, const double* origin, const double* dir, int64_t n, double* t,
                 int32_t* id, double* orient);

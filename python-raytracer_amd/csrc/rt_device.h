@@ -37,6 +37,28 @@
 #define RT_HDM inline
 #endif
 
+// Diagnostic build only (-DRT_PROF): wave-time per code section, sampled on 1/16 of the blocks,
+// read back with srt_debug_prof (tools/prof_sections.py).  Compiles to nothing otherwise.
+#if defined(RT_PROF) && defined(__HIPCC__)
+__device__ unsigned long long g_rt_prof[64];
+#endif
+#if defined(RT_PROF) && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint64_t rt_clock() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ void rt_prof_add(int k, uint64_t dt) {
+    if ((blockIdx.x & 15) != 0) return;
+    const uint64_t m = __ballot(1);
+    if ((uint64_t)__lane_id() == (uint64_t)__builtin_ctzll(m)) {
+        atomicAdd(&g_rt_prof[k], (unsigned long long)dt);
+        atomicAdd(&g_rt_prof[32 + k], 1ull);
+    }
+}
+#define RT_T0(v) const uint64_t v = rt_clock()
+#define RT_ACC(k, v) rt_prof_add(k, rt_clock() - v)
+#else
+#define RT_T0(v)
+#define RT_ACC(k, v)
+#endif
+
 namespace rt {
 
 // constants (reference utils/constants.py:1-4)
@@ -607,6 +629,7 @@ template <class E>
 RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, double orient,
                         E& em, uint32_t& err) {
     const RT_RO srt_material& m = S.mat[mi];
+    RT_T0(tg0);
     d3 P = add(r.o, mul(r.d, t));
     d3 N = shading_normal(S, c, m, P, orient, err);
     d3 diff;
@@ -617,6 +640,8 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
     } else {
         diff = ld3(m.p);
     }
+    RT_ACC(4, tg0);
+    RT_T0(tg1);
     d3 color = mul(ld3(S.ambient), diff);
     d3 V = mul(r.d, -1.0);
     d3 nudged = add(P, mul(N, NUDGE));
@@ -643,7 +668,9 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
 #else
         if (S.nshadow > 0) {
 #endif
+            RT_T0(ts0);
             double ln = shadow_nearest(S, l, nudged, L);
+            RT_ACC(5, ts0);
             seelight = (ln >= dist) ? 1.0 : 0.0;
             em.shadow(1);
         }
@@ -656,7 +683,9 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
 #ifdef RT_ABL_POW  // diagnostic build only
             double Dphong = (pow5(np_clip(dot(N, H), 0.0, 1.0)) * m.p[5]) / m.p[6];
 #else
+            RT_T0(tp0);
             double Dphong = (pow(np_clip(dot(N, H), 0.0, 1.0), m.p[4]) * m.p[5]) / m.p[6];
+            RT_ACC(6, tp0);
 #endif
             double den = 4.0 * np_clip(dot(N, V) * NdotL, 0.001, 1.0);
             const Quot qd(den);
@@ -665,14 +694,20 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
             color = add(color, spec);
         }
     }
+    RT_ACC(7, tg1);
     em.local(color);
 #ifdef RT_ABL_NOEMIT  // diagnostic build only
     return;
 #endif
     if ((int)meta_depth(r.meta) < c.max_ray_depth) {
+        RT_T0(tc0);
         double cos_t = np_clip(dot(V, N), 0.0, 1.0);
         d3 F = schlick(ld3(m.p + 8), cos_t);
-        em.child(mkchild(nudged, reflect_dir(r.d, N), F, med, meta_diffuse(r.meta), 1));
+        Child ch = mkchild(nudged, reflect_dir(r.d, N), F, med, meta_diffuse(r.meta), 1);
+        RT_ACC(8, tc0);
+        RT_T0(tc1);
+        em.child(ch);
+        RT_ACC(9, tc1);
     }
 }
 
@@ -777,10 +812,14 @@ RT_HD void shade_sky(const SceneView& S, const RT_RO srt_collider& c, int mi, co
     return;
 #endif
     const RT_RO srt_material& m = S.mat[mi];
+    RT_T0(tk0);
     d3 P = add(r.o, mul(r.d, t));
     double u, v;
     if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+    RT_ACC(10, tk0);
+    RT_T0(tk1);
     d3 col = tex_rgb(S, m.tex, u, v, err);
+    RT_ACC(11, tk1);
     if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP)) {
         const RT_RO srt_texture& L = S.tex[m.tex_aux0];
         const RT_RO uint8_t* px = tex_uv(S, L, u, v, err);

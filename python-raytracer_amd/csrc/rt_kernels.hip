@@ -55,7 +55,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 600;
+constexpr size_t TRACE_PARAMS_BYTES = 752;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 
 struct Queue {
@@ -84,7 +84,20 @@ struct TraceParams {
     const double* jitter;  // [spp][4][npix] (device) or null
     int sample_base;
     int spp;           // samples of this pass (k_primary)
+    int spt;           // samples per thread: k_primary item i = (pixel i % npix, samples [g*spt, g*spt+spt)),
+                       // g = i / npix; spt < spp (small frames) adds to a zeroed framebuffer with atomics
+    int pad_;
     int32_t* hit_out;  // [spp][npix] or null
+    // frame kernel (k_frame): per-wave ray rings in HBM, slot s = rays [s * ring_cap, (s+1) * ring_cap)
+    Queue ring;
+    uint32_t* ring_lock;  // [nslot] 0 = free, 1 = owned by a running wave
+    int64_t ring_cap;     // rays per ring (power of two)
+    double* out_rgb;      // fused resolve (single-pass frames): [3][npix] linear RGB or null
+    uint8_t* out_u8;      //                                     [npix][3] sRGB8 or null
+    int nslot;
+    int dcap;             // deepest depth traced; deeper children are counted and dropped
+    int fuse_resolve;     // 1: k_frame resolves its pixels (no framebuffer); 0: adds to fb
+    int spp_total;        // samples of the frame (resolve average)
 };
 // kernel argument: host and device passes must agree on the layout (catches address-space pointer
 // size differences, see SceneView)
@@ -186,7 +199,7 @@ struct GpuEmit {
         for (int k = 0; k < g.count; ++k) {
             Rng rng;
             const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(P.seed, r.pix, cpath, 0xD1000000u | (uint32_t)P.depth);
+            rng.init(P.seed, r.pix, cpath, 0xD1000000u | meta_depth(r.meta));
             store(slot + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
         }
     }
@@ -195,7 +208,7 @@ struct GpuEmit {
 __device__ __forceinline__ double mc_uniform(const TraceParams& P, const Ray& r, int cid, uint32_t round) {
     if (!(P.S.col[cid].flags & SRT_CF_MC)) return 0.0;
     Rng g;
-    g.init(P.seed, r.pix, r.path, 0x3C000000u | ((uint32_t)P.depth << 8) | round);
+    g.init(P.seed, r.pix, r.path, 0x3C000000u | (meta_depth(r.meta) << 8) | round);
     return g.one();
 }
 
@@ -215,16 +228,20 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
 
 // One trace step for one ray (all lanes of the wave call it; `active` masks the tail).
 // MATS: material types compiled into this instantiation (the host picks one covering the scene).
-template <uint32_t MATS>
-__device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool active, uint32_t shard, uint32_t& err,
-                                          uint32_t& shadow, int32_t* hit_slot, d3* acc) {
+// Em: the emitter (GpuEmit: wavefront queues; FrameEmit: the frame kernel's per-wave ring); `em0`
+// is round 0's, tied colliders get copies with rounds 1, 2, ...
+template <uint32_t MATS, class Em>
+__device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool active, uint32_t& err, int32_t* hit_slot,
+                                          const Em& em0) {
     const SceneView& S = P.S;
     double t = FARAWAY, o = FARAWAY;
     bool ties = false;
     int id = -1;
+    RT_T0(tn0);
     if (active) id = nearest_hit(S, r.o, r.d, t, o, ties);
+    RT_ACC(1, tn0);
     if (hit_slot && active) *hit_slot = id;
-    GpuEmit em{P, r, shard, 0u, &shadow, acc};
+    const Em& em = em0;
 #ifdef RT_ABL_NOSHADE  // diagnostic build only: raygen + nearest hit, no shading
     if (id == 12345) em.local(d3{t, o, 0.0});
     return;
@@ -232,8 +249,10 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     // waterfall over the colliders hit in this wave: inside each pass the collider index, and so
     // its material and every table entry they reference, is wave-uniform (scalar loads into SGPRs,
     // uniform branches); a wave usually sees one to three distinct colliders
+    RT_T0(tw0);
     uint64_t pending = __ballot(id >= 0);
     while (pending) {
+        RT_ACC(12, tw0);  // counts waterfall passes (k = 12 calls)
         const int lead = __builtin_ctzll(pending);
         const int cu = __builtin_amdgcn_readfirstlane(__shfl(id, lead));
         const bool mine = (id == cu);
@@ -268,6 +287,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         }
         pending &= ~__ballot(mine);
     }
+    RT_ACC(2, tw0);
     // colliders tied at the same distance are all shaded and their colours added (ray.py:131-146)
     if (__ballot(ties)) {
         // wave-uniform collider loop (scalar table loads); lanes act on later colliders at t
@@ -275,7 +295,8 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         for (int c = 0; c < S.ncol; ++c) {
             double oc;
             if (ties && c > id && collider_hit(S.col[c], r.o, r.d, oc) == t) {
-                GpuEmit et{P, r, shard, round++, &shadow, acc};
+                Em et = em0;
+                et.round = round++;
                 shade_hit<MATS>(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(P, r, c, round - 1));
             }
         }
@@ -302,11 +323,14 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
     uint32_t shadow = 0;
-    const int64_t n = P.npix;
+    const int64_t ngroups = (P.spp + P.spt - 1) / P.spt;
+    const int64_t n = P.npix * ngroups;
     for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
         const int64_t i = base + threadIdx.x;
         const bool active = i < n;
-        const uint32_t p = active ? (uint32_t)i : 0u;
+        const int64_t grp = active ? i / P.npix : 0;
+        const uint32_t p = active ? (uint32_t)(i - grp * P.npix) : 0u;
+        const int s_begin = (int)grp * P.spt, s_end = min(P.spp, s_begin + P.spt);
         const uint32_t lr = p / (uint32_t)P.cam.width;
         const uint32_t col = p - lr * (uint32_t)P.cam.width;
         const int grow = active ? P.rows[lr] : 0;
@@ -315,8 +339,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
         // software pipeline: the next sample's uniforms are loaded while this sample is traced
         double jn[4] = {0.0, 0.0, 0.0, 0.0};
-        if (active) primary_uniforms(P, 0, p, gpix, jn);
-        for (int s = 0; s < P.spp; ++s) {
+        if (active) primary_uniforms(P, s_begin, p, gpix, jn);
+        for (int s = s_begin; s < s_end; ++s) {
             Ray r;
             r.o = r.d = d3{0.0, 0.0, 0.0};
             r.w = d3{1.0, 1.0, 1.0};
@@ -324,12 +348,18 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             r.pix = p;
             r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
             const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
-            if (active && s + 1 < P.spp) primary_uniforms(P, s + 1, p, gpix, jn);
+            RT_T0(tr0);
+            if (active && s + 1 < s_end) primary_uniforms(P, s + 1, p, gpix, jn);
             if (active) primary_ray(P.cam, xc, yr, j, r.o, r.d);
+            RT_ACC(0, tr0);
             int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
-            trace_one<MATS>(P, r, active, shard, err, shadow, hs, &acc);
+            RT_T0(tt0);
+            trace_one<MATS>(P, r, active, err, hs, GpuEmit{P, r, shard, 0u, &shadow, &acc});
+            RT_ACC(3, tt0);
         }
-        if (active && P.fb_first) {
+        if (ngroups > 1) {
+            if (active) fb_add(P.fb, P.npix, p, d3{1.0, 1.0, 1.0}, acc);
+        } else if (active && P.fb_first) {
             P.fb[p] = acc.x;
             P.fb[P.npix + p] = acc.y;
             P.fb[2 * P.npix + p] = acc.z;
@@ -359,16 +389,231 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
         const int64_t i = base + threadIdx.x;
         const bool active = i < n;
         Ray r;
+        RT_T0(tq0);
         if (active) {
             r = queue_load(P.qin, off + i);
         } else {
             r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
             r.pix = 0; r.meta = 0; r.path = 0;
         }
-        trace_one<MATS>(P, r, active, shard, err, shadow, nullptr, nullptr);
+        RT_ACC(13, tq0);
+        RT_T0(tt1);
+        trace_one<MATS>(P, r, active, err, nullptr, GpuEmit{P, r, shard, 0u, &shadow, nullptr});
+        RT_ACC(14, tt1);
     }
     if (err) atomicOr(&P.flags[0], err);
     if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+}
+
+// ---- the frame kernel ----------------------------------------------------------------------
+// One wave (a 64-thread block) owns a tile of 64 consecutive pixels and traces their whole ray
+// trees: it generates the tile's primary rays sample by sample, appends every child to a private
+// ring in HBM and drains the ring in FIFO order, taking a full 64-ray chunk whenever one is
+// pending and new primaries otherwise.  Colours go to per-pixel accumulators in LDS; at the end
+// the wave writes (or resolves) its 64 pixels.  No atomics between waves, no per-depth launches:
+// the depth tails of different tiles overlap on the GPU instead of serialising kernel after
+// kernel, and all samples of a pixel are queued together, which keeps lanes ~95 % busy
+// (simulated on the ex1 1080p path-length distribution: 94.6 % with pure chunks).
+constexpr int FRAME_BLOCK = 64;
+
+struct FrameLds {
+    double acc[3][FRAME_BLOCK];  // per-pixel colour sums of the tile
+    uint32_t depth_cnt[SRT_MAX_DEPTHS];
+    uint32_t head, tail;         // ring positions (wave-uniform; kept in LDS so that updates made
+                                 // under divergent control flow are seen by every lane)
+    uint32_t slot;
+    uint32_t overflow;
+};
+
+// The ring positions are shared by the wave's lanes through LDS.  Plain loads/stores would let the
+// compiler forward a lane's own earlier value past another lane's update (a data race under the
+// single-thread model), so every access is an atomic at workgroup scope and the reserving lane's
+// result is broadcast with a cross-lane read.
+__device__ __forceinline__ uint32_t lds_get(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct FrameEmit {
+    const TraceParams& P;
+    const Ray& r;
+    uint32_t round;
+    uint32_t* shadow_acc;
+    FrameLds* L;
+    uint32_t tile0;
+    int64_t ring_base;
+
+    __device__ void local(d3 c) const {
+        if (is_zero(c)) return;
+        const uint32_t k = r.pix - tile0;
+        __hip_atomic_fetch_add(&L->acc[0][k], r.w.x * c.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&L->acc[1][k], r.w.y * c.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&L->acc[2][k], r.w.z * c.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
+    // `cnt` consecutive ring positions for every active lane (wave-local: LDS counter, no atomics)
+    __device__ uint32_t reserve(uint32_t cnt) const {
+        uint32_t total = 0, below = 0;
+        for (int b = 0; b < 8; ++b) {
+            uint64_t m = __ballot((cnt >> b) & 1u);
+            total += (uint32_t)__builtin_popcountll(m) << b;
+            below += lanes_below(m) << b;
+        }
+        const uint64_t act = __ballot(1);
+        const int leader = __builtin_ctzll(act);
+        uint32_t base = 0;
+        if (lanes_below(act) == 0)
+            base = __hip_atomic_fetch_add(&L->tail, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        base = (uint32_t)__shfl((int)base, leader);
+        return base + below;
+    }
+    __device__ void store(uint32_t pos, const Child& c, uint32_t path) const {
+        const uint32_t depth = meta_depth(r.meta) + 1;
+        if (pos - lds_get(&L->head) >= (uint32_t)P.ring_cap) {  // ring full: the frame is re-rendered with bigger rings
+            lds_put(&L->overflow, 1u);
+            return;
+        }
+        queue_store(P.ring, ring_base + (int64_t)(pos & (uint32_t)(P.ring_cap - 1)), c.o, c.d, mul(r.w, c.w), r.pix,
+                    pack_meta(c.medium, depth, c.dfl), path);
+    }
+    __device__ void child(const Child& c) const {
+        store(reserve(1u), c, child_path(r.path, c.slot, round));
+    }
+    __device__ void diffuse(const DiffuseGen& g, int mi) const {
+        const uint32_t pos = reserve((uint32_t)g.count);
+        const auto& m = P.S.mat[mi];
+        for (int k = 0; k < g.count; ++k) {
+            Rng rng;
+            const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
+            rng.init(P.seed, r.pix, cpath, 0xD1000000u | meta_depth(r.meta));
+            store(pos + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
+        }
+    }
+};
+
+template <uint32_t MATS, int OCC = 2>
+__global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
+    TraceParams P = P0;
+    {
+        extern __shared__ double lds_lut[];
+        const int nl = P.S.nlut_lds;
+        for (int i = threadIdx.x; i < nl * 256; i += FRAME_BLOCK) lds_lut[i] = P.S.tex[i >> 8].lut[i & 255];
+        P.S.lut_lds = (const RT_LDS double*)lds_lut;
+    }
+    __shared__ FrameLds L;
+    RT_T0(tf0);
+    const uint32_t lane = threadIdx.x;
+    for (int k = 0; k < 3; ++k) L.acc[k][lane] = 0.0;
+    for (int d = lane; d < SRT_MAX_DEPTHS; d += FRAME_BLOCK) L.depth_cnt[d] = 0u;
+    if (lane == 0) {
+        // a free ring: slots are tried from blockIdx on; there are twice as many as resident waves
+        uint32_t s = blockIdx.x % (uint32_t)P.nslot;
+        while (atomicCAS(&P.ring_lock[s], 0u, 1u) != 0u) s = (s + 1u) % (uint32_t)P.nslot;
+        L.slot = s;
+        L.head = 0u;
+        L.tail = 0u;
+        L.overflow = 0u;
+    }
+    __syncthreads();
+    RT_ACC(18, tf0);
+    const uint32_t tile0 = blockIdx.x * FRAME_BLOCK;
+    const int64_t ring_base = (int64_t)L.slot * P.ring_cap;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    uint32_t err = 0;
+    uint32_t shadow = 0;
+    // this lane's pixel of the tile
+    const uint32_t p = tile0 + lane;
+    const bool pact = p < (uint32_t)P.npix;
+    const uint32_t lr = pact ? p / (uint32_t)P.cam.width : 0u;
+    const uint32_t col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
+    const int grow = pact ? P.rows[lr] : 0;
+    const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
+    const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
+    int s_next = 0;
+    for (;;) {
+        const uint32_t head = lds_get(&L.head), tail = lds_get(&L.tail);
+        const uint32_t pending = tail - head;
+        if (pending == 0u && s_next >= P.spp) break;
+        Ray r;
+        bool active;
+        uint32_t depth = 0;
+        int32_t* hs = nullptr;
+        if (pending >= (uint32_t)FRAME_BLOCK || s_next >= P.spp) {
+            // a chunk of the ring
+            const uint32_t take = min(pending, (uint32_t)FRAME_BLOCK);
+            active = lane < take;
+            RT_T0(tl0);
+            if (active) {
+                r = queue_load(P.ring, ring_base + (int64_t)((head + lane) & (uint32_t)(P.ring_cap - 1)));
+                depth = meta_depth(r.meta);
+            } else {
+                r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
+                r.pix = tile0; r.meta = 0; r.path = 0;
+            }
+            if (lane == 0) lds_put(&L.head, head + take);
+            RT_ACC(16, tl0);
+        } else {
+            // primary rays of sample s_next for the tile's pixels (camera.py:51-85)
+            const int s = s_next++;
+            active = pact;
+            r.o = r.d = d3{0.0, 0.0, 0.0};
+            r.w = d3{1.0, 1.0, 1.0};
+            r.meta = pack_meta(0, 0, 0);
+            r.pix = pact ? p : tile0;
+            r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
+            RT_T0(tg0);
+            if (active) {
+                double j[4];
+                primary_uniforms(P, s, p, gpix, j);
+                primary_ray(P.cam, xc, yr, j, r.o, r.d);
+            }
+            RT_ACC(15, tg0);
+            if (P.hit_out && active) hs = P.hit_out + (int64_t)s * P.npix + p;
+        }
+        // rays entering each depth; a ray beyond the depth cap is counted (the host reports it as an
+        // error) and dropped, so every ring drains
+        if (active) {
+            __hip_atomic_fetch_add(&L.depth_cnt[min(depth, (uint32_t)SRT_MAX_DEPTHS - 1u)], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((int)depth > P.dcap) active = false;
+        }
+        RT_T0(tt2);
+        trace_one<MATS>(P, r, active, err, hs, FrameEmit{P, r, 0u, &shadow, &L, tile0, ring_base});
+        RT_ACC(17, tt2);
+    }
+    RT_T0(te0);
+    // tile pixels out
+    if (pact) {
+        const double ar = L.acc[0][lane], ag = L.acc[1][lane], ab = L.acc[2][lane];
+        if (P.fuse_resolve) {
+            const double spp = (double)P.spp_total;
+            double rr = ar / spp, gg = ag / spp, bb = ab / spp;
+            uint8_t px[3];
+            double a0, a1, a2;
+            resolve_pixel(rr, gg, bb, a0, a1, a2, px);
+            if (P.out_rgb) { P.out_rgb[p] = rr; P.out_rgb[P.npix + p] = gg; P.out_rgb[2 * P.npix + p] = bb; }
+            if (P.out_u8) { P.out_u8[3 * p] = px[0]; P.out_u8[3 * p + 1] = px[1]; P.out_u8[3 * p + 2] = px[2]; }
+        } else if (P.fb_first) {
+            P.fb[p] = ar; P.fb[P.npix + p] = ag; P.fb[2 * P.npix + p] = ab;
+        } else {
+            P.fb[p] += ar; P.fb[P.npix + p] += ag; P.fb[2 * P.npix + p] += ab;
+        }
+    }
+    __syncthreads();
+    for (int d = lane; d <= P.dcap + 1 && d < SRT_MAX_DEPTHS; d += FRAME_BLOCK)
+        if (L.depth_cnt[d]) atomicAdd(P.cnt_out + (int64_t)d * NSHARD + shard, L.depth_cnt[d]);
+    if (err) atomicOr(&P.flags[0], err);
+    if (lane == 0 && lds_get(&L.overflow)) atomicOr(&P.flags[1], 1u);
+    // the wave's shadow-ray count into its shard's counter
+    for (int off = 32; off > 0; off >>= 1) shadow += __shfl_xor(shadow, off);
+    if (lane == 0) {
+        if (shadow) atomicAdd(P.shadow + shard, (unsigned long long)shadow);
+        __threadfence();
+        atomicExch(&P.ring_lock[L.slot], 0u);
+    }
+    RT_ACC(19, te0);
 }
 
 // Kernel variants by the material types they contain; the host picks the first covering the scene.
@@ -380,21 +625,22 @@ struct Variant {
     uint32_t mats;
     void (*primary)(TraceParams);
     void (*trace)(TraceParams);
+    void (*frame)(TraceParams);
 };
 // occupancy experiments for the headline scene (srt_set_option "occupancy" = 1 (index 2), 3, 4);
 // the default instantiations use 2 waves/SIMD, the fastest measured (profiles/)
 const Variant OCC_VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>},
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>},
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>, k_frame<MATS_GLOSSY_SKY, 1>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>, k_frame<MATS_GLOSSY_SKY, 3>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>, k_frame<MATS_GLOSSY_SKY, 4>},
 };
 int g_occupancy = 0;
 const Variant VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>},
-    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC>},
-    {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>},
-    {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>},
-    {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>, k_frame<MATS_GLOSSY_SKY>},
+    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC>, k_frame<MATS_DIELECTRIC>},
+    {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>, k_frame<MATS_FILM>},
+    {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>, k_frame<MATS_MC>},
+    {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>, k_frame<MAT_ALL>},
 };
 const Variant& pick_variant(uint32_t mats) {
     if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
@@ -403,8 +649,34 @@ const Variant& pick_variant(uint32_t mats) {
     return VARIANTS[sizeof(VARIANTS) / sizeof(VARIANTS[0]) - 1];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npix, double inv_spp_div, double spp,
-                                                  double* rgb, uint8_t* u8) {
+// End of a pass (one block): hand the per-depth append counters and the error/overflow flags to
+// the host through pinned memory and zero them for the next pass (replaces two memsets and two
+// copies per pass; the frame's stream needs no host round trip until its end).
+__global__ __launch_bounds__(BLOCK) void k_pass_end(uint32_t* counts, int64_t words, uint32_t* flags,
+                                                   uint32_t* host, uint32_t* host_flags) {
+    for (int64_t i = threadIdx.x; i < words; i += BLOCK) {
+        host[i] = counts[i];
+        counts[i] = 0u;
+    }
+    if (threadIdx.x < 2) {
+        host_flags[threadIdx.x] |= flags[threadIdx.x];  // accumulated until the host checks them
+        flags[threadIdx.x] = 0u;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npix, unsigned long long* shadow,
+                                                  uint32_t* shadow_host, double spp, double* rgb, uint8_t* u8) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // the frame's shadow-ray count (NSHARD counters) to the host, zeroed for the next frame (no
+        // kernel of this frame adds to them any more)
+        unsigned long long v = 0;
+        for (int k = 0; k < NSHARD; ++k) {
+            v += shadow[k];
+            shadow[k] = 0ull;
+        }
+        shadow_host[0] = (uint32_t)v;
+        shadow_host[1] = (uint32_t)(v >> 32);
+    }
     for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK) {
         double r = fb[p] / spp, g = fb[npix + p] / spp, b = fb[2 * npix + p] / spp;
         uint8_t px[3];
@@ -413,7 +685,6 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npi
         if (rgb) { rgb[p] = r; rgb[npix + p] = g; rgb[2 * npix + p] = b; }
         if (u8) { u8[3 * p] = px[0]; u8[3 * p + 1] = px[1]; u8[3 * p + 2] = px[2]; }
     }
-    (void)inv_spp_div;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O, const double* D, int64_t n, double* t,
@@ -644,6 +915,14 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
 
 }  // namespace
 
+// shape of one frame's passes (what the read-back of its counters needs)
+struct FramePlan {
+    bool frame = false;  // rendered by k_frame (counts are totals, not queue fills)
+    int64_t npix = 0;
+    int spp = 0, batch = 0, npass = 0, dcap = 0, nev = 0;
+    int64_t cnt_words = 0, pass_words = 0;
+};
+
 struct srt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -686,6 +965,24 @@ struct srt_ctx {
     int64_t mt_out_cap = 0;
     uint32_t* host = nullptr;  // pinned: per-pass counters/flags, shadow count
     int64_t host_words = 0;
+    // counts/flags/shadow are zeroed by the kernels that consume them (k_pass_end, k_resolve); a
+    // frame that did not complete leaves them dirty and the next one clears them first
+    bool dirty = true;
+    // frame kernel rings (k_frame): nslot rings of ring_cap rays, one lock word per ring
+    // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
+    // per-depth wavefront kernels otherwise.  Measured (one MI355X, Mrays/s, wavefront vs frame):
+    // ex1 1080p d5 13388 vs 10478, ex3 1080p d8 8950 vs 9585, ex4 4K d6 14081 vs 17494,
+    // cornell 800x800 512 spp 3542 vs 4073.
+    int use_frame = -1;
+    Queue ring{};
+    int64_t ring_cap = 0;
+    int nslot = 0;
+    uint32_t* ring_lock = nullptr;
+    std::vector<void*> ring_bufs;
+    // asynchronous frames (SRT_RENDER_ASYNC) in flight since the last synchronisation point
+    int async_pending = 0;
+    FramePlan async_plan;
+    srt_stats async_stats{};
 };
 
 namespace {
@@ -718,6 +1015,38 @@ int ensure_queues(srt_ctx* c, int64_t rays) {
         }
     }
     c->seg = seg;
+    return SRT_OK;
+}
+
+// rings of the frame kernel: more rings than waves can ever be resident (32 per CU), so a wave
+// always finds a free one; `cap` rays each (power of two)
+int ensure_ring(srt_ctx* c, int64_t cap) {
+    int64_t k = 256;
+    while (k < cap) k <<= 1;
+    cap = k;
+    int dev_cus = c->max_blocks / 8;
+    const int nslot = std::max(1024, 2 * 32 * dev_cus);
+    if (cap <= c->ring_cap && nslot <= c->nslot) return SRT_OK;
+    free_list(c->ring_bufs);
+    c->ring_cap = 0;
+    c->nslot = 0;
+    const int64_t n = cap * nslot;
+    Queue& q = c->ring;
+    double** dptr[9] = {&q.ox, &q.oy, &q.oz, &q.dx, &q.dy, &q.dz, &q.wr, &q.wg, &q.wb};
+    for (double** p : dptr) {
+        if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray ring allocation failed");
+        c->ring_bufs.push_back(*p);
+    }
+    uint32_t** uptr[3] = {&q.pix, &q.meta, &q.path};
+    for (uint32_t** p : uptr) {
+        if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray ring allocation failed");
+        c->ring_bufs.push_back(*p);
+    }
+    if (dalloc(&c->ring_lock, nslot) != hipSuccess) return fail(SRT_ERR_MEMORY, "ring lock allocation failed");
+    c->ring_bufs.push_back(c->ring_lock);
+    HIP_TRY(hipMemset(c->ring_lock, 0, (size_t)nslot * 4));
+    c->ring_cap = cap;
+    c->nslot = nslot;
     return SRT_OK;
 }
 
@@ -800,6 +1129,89 @@ int64_t depth_total(const uint32_t* cnt, int64_t seg) {
 
 }  // namespace
 
+namespace {
+
+// Read back a completed frame (its stream has been synchronised): error/overflow flags OR-ed over
+// every pass (and every asynchronous frame since the last synchronisation point), per-depth counts
+// and kernel times of the frame's passes.  Returns SRT_RETRY_OVERFLOW when a queue shard overflowed.
+constexpr int SRT_RETRY_OVERFLOW = 1;
+int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
+    bool overflow = false;
+    for (int p = 0; p < F.npass; ++p) {
+        const uint32_t* hp = c->host + p * F.pass_words;
+        int rc;
+        if ((rc = check_flags(hp[F.cnt_words]))) return rc;
+        overflow |= hp[F.cnt_words + 1] != 0;
+    }
+    if (overflow) return SRT_RETRY_OVERFLOW;
+    double ms_trace = 0.0, ms_primary = 0.0;
+    for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.rays_per_depth[d] = 0;
+    for (int p = 0; p < F.npass; ++p) {
+        const uint32_t* hp = c->host + p * F.pass_words;
+        if (depth_total(hp + (int64_t)(F.dcap + 1) * NSHARD, F.frame ? INT64_MAX : c->seg) != 0)
+            return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
+        if (F.frame) {
+            // k_frame counts every ray it traces (per shard), depth 0 included
+            for (int d = 0; d <= F.dcap; ++d)
+                for (int k = 0; k < NSHARD; ++k) S.rays_per_depth[d] += hp[(int64_t)d * NSHARD + k];
+        } else {
+            S.rays_per_depth[0] += (int64_t)std::min(F.batch, F.spp - p * F.batch) * F.npix;
+            for (int d = 1; d <= F.dcap; ++d) S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, c->seg);
+        }
+        const hipEvent_t* ev = c->ev.data() + (int64_t)p * F.nev;
+        float ms;
+        HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        ms_primary += ms;
+        HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[F.dcap + 1]));
+        ms_trace += ms;
+    }
+    const uint32_t* hshadow = c->host + F.npass * F.pass_words;
+    S.passes = F.npass;
+    S.ms_trace_kernels = ms_trace;
+    S.ms_primary_kernel = ms_primary;
+    S.ms_device = ms_trace;
+    S.shadow_rays = (int64_t)(hshadow[0] | (uint64_t)hshadow[1] << 32);
+    S.n_depths = F.dcap + 1;
+    S.total_rays = 0;
+    for (int d = 0; d <= F.dcap; ++d) S.total_rays += S.rays_per_depth[d];
+    return SRT_OK;
+}
+
+// zero the pinned flag words of every pass (only while no frame is in flight)
+void clear_host_flags(srt_ctx* c, const FramePlan& F) {
+    for (int p = 0; p < F.npass; ++p) {
+        c->host[p * F.pass_words + F.cnt_words] = 0u;
+        c->host[p * F.pass_words + F.cnt_words + 1] = 0u;
+    }
+}
+
+// Wait for the asynchronous frames in flight and check them (flags accumulated over all of them,
+// stats of the last).  An overflow grows the queues and is reported as an error: those frames are
+// wrong and must be rendered again.
+int finish_async(srt_ctx* c, srt_stats* st) {
+    if (c->async_pending == 0) {
+        if (st) *st = c->async_stats;
+        return SRT_OK;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->async_pending = 0;
+    srt_stats S{};
+    int rc = collect_frame(c, c->async_plan, S);
+    clear_host_flags(c, c->async_plan);
+    if (rc == SRT_RETRY_OVERFLOW) {
+        if ((rc = c->async_plan.frame ? ensure_ring(c, 2 * c->ring_cap) : ensure_queues(c, 2 * c->seg * NSHARD)))
+            return rc;
+        return fail(SRT_ERR_MEMORY, "a ray queue overflowed during an asynchronous frame (queues grown; render "
+                                    "that frame again)");
+    }
+    if (rc) return rc;
+    c->async_stats = S;
+    if (st) *st = S;
+    return SRT_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int srt_abi_version(void) { return SRT_ABI_VERSION; }
@@ -830,7 +1242,7 @@ int srt_create(int device, srt_ctx** out) {
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(dalloc(&c->counts, SRT_MAX_DEPTHS * NSHARD));
     HIP_TRY(dalloc(&c->flags, 2));
-    HIP_TRY(dalloc(&c->shadow, 1));
+    HIP_TRY(dalloc(&c->shadow, NSHARD));
     *out = c;
     return SRT_OK;
 }
@@ -841,6 +1253,7 @@ int srt_destroy(srt_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     free_list(c->scene_bufs);
     free_list(c->queue_bufs);
+    free_list(c->ring_bufs);
     void* bufs[] = {c->fb, c->rgb, c->u8, c->xs, c->ys, c->rows, c->jit, c->hit, c->counts, c->flags, c->shadow,
                     c->mt, c->mt_out};
     for (void* p : bufs)
@@ -856,6 +1269,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
     if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
     if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
+    if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
     return fail(SRT_ERR_ARG, std::string("unknown option ") + key);
 }
@@ -894,6 +1308,8 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
         if (m.type == SRT_DIFFUSE && (m.ival < 1 || m.ival > 255)) return fail(SRT_ERR_ARG, "diffuse_rays must be 1..255");
     }
     HIP_TRY(hipSetDevice(c->device));
+    int rc0 = finish_async(c, nullptr);  // frames in flight read the scene tables freed below
+    if (rc0) return rc0;
     HIP_TRY(hipStreamSynchronize(c->stream));
     free_list(c->scene_bufs);
     c->has_scene = false;
@@ -943,12 +1359,15 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     return SRT_OK;
 }
 
+
 int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
     if (a->spp <= 0 || cam->width <= 0 || cam->height <= 0 || a->n_rows <= 0 || !cam->xs || !cam->ys)
         return fail(SRT_ERR_ARG, "spp, width, height, n_rows must be positive and xs/ys set");
+    if (a->flags & ~SRT_RENDER_ASYNC) return fail(SRT_ERR_ARG, "unknown render flag");
+    const bool async = (a->flags & SRT_RENDER_ASYNC) != 0;
     std::vector<int32_t> rows_h;
     if (a->rows) {
         if (is_device_ptr(a->rows)) return fail(SRT_ERR_ARG, "rows must be host memory");
@@ -963,7 +1382,40 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     const int64_t W = cam->width;
     const int64_t npix = (int64_t)a->n_rows * W;
     if (npix >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "image too large");
+    const bool jit_dev = is_device_ptr(a->jitter);
+    const bool hit_dev = is_device_ptr(a->out_hit_id);
+    const bool rgb_dev = is_device_ptr(a->out_rgb), u8_dev = is_device_ptr(a->out_srgb8);
+    if (async && ((a->jitter && !jit_dev) || (a->out_hit_id && !hit_dev) || (a->out_rgb && !rgb_dev) ||
+                  (a->out_srgb8 && !u8_dev)))
+        return fail(SRT_ERR_ARG, "an asynchronous render takes device (or NULL) jitter and outputs");
     int rc;
+    // samples per pass: both queues must hold spp_pass * npix * fanout rays
+    const int64_t per_sample = npix * c->fanout;
+    const int64_t budget_rays = c->queue_budget / (2 * RAY_BYTES);
+    int batch = a->batch_spp > 0 ? a->batch_spp
+                                 : (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, budget_rays / per_sample));
+    batch = std::min(batch, a->spp);
+    while (batch > 1 && (int64_t)batch * npix * c->fanout >= ((int64_t)1 << 32) - 1) batch /= 2;
+    FramePlan F;
+    F.npix = npix;
+    F.spp = a->spp;
+    F.batch = batch;
+    F.npass = (a->spp + batch - 1) / batch;
+    F.dcap = depth_cap(c);
+    F.nev = F.dcap + 2;  // events per pass: before k_primary, after each depth
+    F.cnt_words = (int64_t)SRT_MAX_DEPTHS * NSHARD;
+    F.pass_words = F.cnt_words + 2;
+    F.frame = c->use_frame < 0 ? c->fanout > 1 : c->use_frame != 0;
+    // frames in flight use the buffers below: a synchronous frame, or one that would reallocate
+    // anything, first waits for them (and reports their errors)
+    if (c->async_pending > 0) {
+        const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && a->n_rows <= c->cam_cap[2] &&
+                          3 * npix <= c->fb_cap && 3 * npix <= c->rgb_cap && 3 * npix <= c->u8_cap &&
+                          (int64_t)batch * npix * c->fanout <= c->seg * NSHARD && F.npass == c->async_plan.npass &&
+                          F.dcap == c->async_plan.dcap && F.frame == c->async_plan.frame;
+        if (!async || !same)
+            if ((rc = finish_async(c, nullptr))) return rc;
+    }
     {
         const void* old[3] = {c->xs, c->ys, c->rows};
         if ((rc = ensure_buf(&c->xs, c->cam_cap[0], W))) return rc;
@@ -981,50 +1433,61 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     if ((rc = ensure_buf(&c->fb, c->fb_cap, 3 * npix))) return rc;
     if ((rc = ensure_buf(&c->rgb, c->rgb_cap, 3 * npix))) return rc;
     if ((rc = ensure_buf(&c->u8, c->u8_cap, 3 * npix))) return rc;
-    // samples per pass: both queues must hold spp_pass * npix * fanout rays
-    const int64_t per_sample = npix * c->fanout;
-    const int64_t budget_rays = c->queue_budget / (2 * RAY_BYTES);
-    int batch = a->batch_spp > 0 ? a->batch_spp
-                                 : (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, budget_rays / per_sample));
-    batch = std::min(batch, a->spp);
-    while (batch > 1 && (int64_t)batch * npix * c->fanout >= ((int64_t)1 << 32) - 1) batch /= 2;
-    const bool jit_dev = is_device_ptr(a->jitter);
     if (a->jitter && !jit_dev && (rc = ensure_buf(&c->jit, c->jit_cap, (int64_t)batch * 4 * npix))) return rc;
-    const bool hit_dev = is_device_ptr(a->out_hit_id);
     if (a->out_hit_id && !hit_dev && (rc = ensure_buf(&c->hit, c->hit_cap, (int64_t)batch * npix))) return rc;
-    if ((rc = ensure_queues(c, (int64_t)batch * npix * c->fanout))) return rc;
-    const int dcap = depth_cap(c);
-    const int npass = (a->spp + batch - 1) / batch;
-    const int nev = dcap + 2;  // events per pass: before k_primary, after each depth
-    if ((int)c->ev.size() < npass * nev) {
+    if (F.frame) {
+        if ((rc = ensure_ring(c, (int64_t)FRAME_BLOCK * (c->fanout + 2) * 2))) return rc;
+    } else if ((rc = ensure_queues(c, (int64_t)batch * npix * c->fanout))) {
+        return rc;
+    }
+    if ((int)c->ev.size() < F.npass * F.nev) {
         for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-        c->ev.assign(npass * nev, nullptr);
+        c->ev.assign(F.npass * F.nev, nullptr);
         for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
     }
     // per-pass counters and flags come back through pinned memory once, at the end of the frame:
     // the passes, the resolve and the output copies are queued without a host round trip
-    const int64_t cnt_words = (int64_t)SRT_MAX_DEPTHS * NSHARD;
-    const int64_t pass_words = cnt_words + 2;
-    if (c->host_words < npass * pass_words + 2) {
+    if (c->host_words < F.npass * F.pass_words + 2) {
         if (c->host) (void)hipHostFree(c->host);
         c->host = nullptr;
         c->host_words = 0;
-        HIP_TRY(hipHostMalloc((void**)&c->host, (size_t)(npass * pass_words + 2) * 4, hipHostMallocDefault));
-        c->host_words = npass * pass_words + 2;
+        HIP_TRY(hipHostMalloc((void**)&c->host, (size_t)(F.npass * F.pass_words + 2) * 4, hipHostMallocDefault));
+        c->host_words = F.npass * F.pass_words + 2;
+        memset(c->host, 0, (size_t)c->host_words * 4);  // depths beyond used_words stay zero
     }
-    srt_stats S{};
     const Variant& V = pick_variant(c->mats);
+    // outputs already in device memory are written in place by k_resolve (no copies)
+    double* res_rgb = a->out_rgb ? (rgb_dev ? a->out_rgb : c->rgb) : nullptr;
+    uint8_t* res_u8 = a->out_srgb8 ? (u8_dev ? a->out_srgb8 : c->u8) : nullptr;
+    // only the depths this frame can reach are handed back and cleared per pass
+    const int64_t used_words = std::min<int64_t>(F.cnt_words, (int64_t)(F.dcap + 2) * NSHARD);
+    srt_stats S{};
     for (;;) {
-        HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
-        for (int p = 0; p < npass; ++p) {
+        if (c->async_pending == 0) clear_host_flags(c, F);  // k_pass_end ORs into them
+        if (c->dirty) {
+            HIP_TRY(hipMemsetAsync(c->shadow, 0, 8 * NSHARD, c->stream));
+            HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)F.cnt_words * 4, c->stream));
+            HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
+        }
+        c->dirty = true;
+        for (int p = 0; p < F.npass; ++p) {
             const int s0 = p * batch;
             const int ns = std::min(batch, a->spp - s0);
             const int64_t nrays = (int64_t)ns * npix;
-            HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)cnt_words * 4, c->stream));
-            HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
             TraceParams P = base_params(c, a->seed);
             P.fb = c->fb;
             P.fb_first = (p == 0);  // the first pass's depth-0 kernel stores the framebuffer (no memset)
+            // samples per k_primary thread: all of the pass's (accumulated in registers) unless the
+            // frame has fewer pixels than a quarter of the resident wave slots, then fewer (pixel x
+            // sample-group items, framebuffer atomics on a zeroed framebuffer).  Measured on a
+            // 1/8 shard of ex1 1080p (261k pixels): 6 samples per thread 118 us, 1 sample 133 us, so
+            // only really small frames split.
+            P.spt = ns;
+            {
+                const int64_t want_items = (int64_t)c->max_blocks * 64;
+                while (P.spt > 1 && npix * ((ns + P.spt - 1) / P.spt) < want_items) P.spt = (P.spt + 1) / 2;
+                if (P.spt < ns && p == 0) HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * npix * 8, c->stream));
+            }
             P.npix = npix;
             P.cam = *cam;
             P.cam.xs = c->xs;
@@ -1042,19 +1505,38 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 }
             }
             if (a->out_hit_id) P.hit_out = hit_dev ? a->out_hit_id + (int64_t)s0 * npix : c->hit;
-            hipEvent_t* ev = c->ev.data() + (int64_t)p * nev;
+            hipEvent_t* ev = c->ev.data() + (int64_t)p * F.nev;
+            if (F.frame) {
+                // the whole pass in one launch: one wave per 64-pixel tile
+                P.ring = c->ring;
+                P.ring_lock = c->ring_lock;
+                P.ring_cap = c->ring_cap;
+                P.nslot = c->nslot;
+                P.dcap = F.dcap;
+                P.cnt_out = c->counts;
+                P.fuse_resolve = (F.npass == 1);
+                P.out_rgb = res_rgb;
+                P.out_u8 = res_u8;
+                P.spp_total = a->spp;
+                HIP_TRY(hipEventRecord(ev[0], c->stream));
+                hipLaunchKernelGGL(V.frame, dim3((unsigned)((npix + FRAME_BLOCK - 1) / FRAME_BLOCK)), dim3(FRAME_BLOCK),
+                                   lut_bytes(c), c->stream, P);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipEventRecord(ev[1], c->stream));
+                HIP_TRY(hipEventRecord(ev[F.dcap + 1], c->stream));
+            } else {
             // depth 0: raygen fused with the trace step
             P.depth = 0;
             P.n_primary = nrays;
             P.qout = c->q[1];
             P.cnt_out = c->counts + NSHARD;
             HIP_TRY(hipEventRecord(ev[0], c->stream));
-            hipLaunchKernelGGL(V.primary, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), lut_bytes(c), c->stream,
-                               P);
+            hipLaunchKernelGGL(V.primary, dim3(grid_for(npix * ((ns + P.spt - 1) / P.spt), c->max_blocks)),
+                               dim3(BLOCK), lut_bytes(c), c->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             P.fb_first = 0;
-            for (int d = 1; d <= dcap; ++d) {
+            for (int d = 1; d <= F.dcap; ++d) {
                 P.depth = d;
                 P.qin = c->q[d & 1];
                 P.qout = c->q[(d + 1) & 1];
@@ -1064,64 +1546,66 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 HIP_TRY(hipGetLastError());
                 HIP_TRY(hipEventRecord(ev[1 + d], c->stream));
             }
-            uint32_t* hp = c->host + p * pass_words;
-            HIP_TRY(hipMemcpyAsync(hp, c->counts, (size_t)cnt_words * 4, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipMemcpyAsync(hp + cnt_words, c->flags, 8, hipMemcpyDeviceToHost, c->stream));
+            }
+            uint32_t* hp = c->host + p * F.pass_words;
+            // counters of this pass -> pinned host words [0, used_words) (the unused depths are zero
+            // on the host), flags OR-ed into the two words at [cnt_words, cnt_words + 2)
+            hipLaunchKernelGGL(k_pass_end, dim3(1), dim3(BLOCK), 0, c->stream, c->counts, used_words, c->flags,
+                               hp, hp + F.cnt_words);
+            HIP_TRY(hipGetLastError());
             if (a->out_hit_id && !hit_dev)
                 HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->hit, (size_t)nrays * 4,
                                        hipMemcpyDeviceToHost, c->stream));
         }
-        hipLaunchKernelGGL(k_resolve, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb, npix,
-                           0.0, (double)a->spp, c->rgb, c->u8);
+        uint32_t* hshadow = c->host + F.npass * F.pass_words;
+        // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
+        const bool fused = F.frame && F.npass == 1;
+        hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb,
+                           fused ? (int64_t)0 : npix, c->shadow, hshadow, (double)a->spp, res_rgb, res_u8);
         HIP_TRY(hipGetLastError());
-        if (a->out_rgb)
-            HIP_TRY(hipMemcpyAsync(a->out_rgb, c->rgb, (size_t)3 * npix * 8, hipMemcpyDefault, c->stream));
-        if (a->out_srgb8) HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->u8, (size_t)3 * npix, hipMemcpyDefault, c->stream));
-        uint32_t* hshadow = c->host + npass * pass_words;
-        HIP_TRY(hipMemcpyAsync(hshadow, c->shadow, 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        bool overflow = false;
-        for (int p = 0; p < npass; ++p) {
-            const uint32_t* hp = c->host + p * pass_words;
-            if ((rc = check_flags(hp[cnt_words]))) return rc;
-            overflow |= hp[cnt_words + 1] != 0;
+        c->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
+        if (async) {
+            // stats of this frame (and its errors) come with srt_render_finish
+            c->async_pending++;
+            c->async_plan = F;
+            return SRT_OK;
         }
-        if (overflow) {
+        if (a->out_rgb && !rgb_dev)
+            HIP_TRY(hipMemcpyAsync(a->out_rgb, c->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->stream));
+        if (a->out_srgb8 && !u8_dev)
+            HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->stream));
+        c->dirty = true;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        c->dirty = false;
+        const int64_t retries = S.retries;
+        rc = collect_frame(c, F, S);
+        if (rc == SRT_RETRY_OVERFLOW) {
             // a queue shard overflowed: grow the queues and render the frame again
-            S.retries++;
+            S.retries = retries + 1;
             if (S.retries > 8) return fail(SRT_ERR_MEMORY, "ray queues keep overflowing");
-            if ((rc = ensure_queues(c, 2 * c->seg * NSHARD))) return rc;
+            if ((rc = F.frame ? ensure_ring(c, 2 * c->ring_cap) : ensure_queues(c, 2 * c->seg * NSHARD))) return rc;
             continue;
         }
-        double ms_trace = 0.0, ms_primary = 0.0, ms_device = 0.0;
-        for (int p = 0; p < npass; ++p) {
-            const uint32_t* hp = c->host + p * pass_words;
-            if (depth_total(hp + (int64_t)(dcap + 1) * NSHARD, c->seg) != 0)
-                return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
-            S.rays_per_depth[0] += (int64_t)std::min(batch, a->spp - p * batch) * npix;
-            for (int d = 1; d <= dcap; ++d) S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, c->seg);
-            const hipEvent_t* ev = c->ev.data() + (int64_t)p * nev;
-            float ms;
-            HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
-            ms_primary += ms;
-            HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[dcap + 1]));
-            ms_trace += ms;
-            ms_device += ms;
-        }
-        S.passes = npass;
-        S.ms_trace_kernels = ms_trace;
-        S.ms_primary_kernel = ms_primary;
-        S.ms_device = ms_device;
-        S.shadow_rays = (int64_t)(hshadow[0] | (uint64_t)hshadow[1] << 32);
+        S.retries = retries;
+        if (rc) return rc;
         break;
     }
     if (st) {
-        S.n_depths = dcap + 1;
-        S.total_rays = 0;
-        for (int d = 0; d <= dcap; ++d) S.total_rays += S.rays_per_depth[d];
         S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         *st = S;
     }
+    return SRT_OK;
+}
+
+int srt_render_finish(srt_ctx* c, srt_stats* st) {
+    if (!c) return fail(SRT_ERR_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    return finish_async(c, st);
+}
+
+int srt_stream(srt_ctx* c, void** stream) {
+    if (!c || !stream) return fail(SRT_ERR_ARG, "null argument");
+    *stream = (void*)c->stream;
     return SRT_OK;
 }
 
@@ -1133,6 +1617,9 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
     if (a->n <= 0) return SRT_OK;
     if (a->n >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "batch too large");
     HIP_TRY(hipSetDevice(c->device));
+    int rc0 = finish_async(c, nullptr);
+    if (rc0) return rc0;
+    c->dirty = true;  // counts/flags/shadow are left as this call's memsets and kernels leave them
     const int64_t n = a->n;
     int rc = SRT_OK;
     double *O = nullptr, *D = nullptr;
@@ -1155,7 +1642,7 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
         HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * n * 8, c->stream));
         HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->stream));
         HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
-        HIP_TRY(hipMemsetAsync(c->shadow, 0, 8, c->stream));
+        HIP_TRY(hipMemsetAsync(c->shadow, 0, 8 * NSHARD, c->stream));
         uint32_t seed_counts[NSHARD];
         for (int s = 0; s < NSHARD; ++s) seed_counts[s] = (uint32_t)((n - s + NSHARD - 1) / NSHARD);
         HIP_TRY(hipMemcpyAsync(c->counts + (int64_t)d0 * NSHARD, seed_counts, sizeof(seed_counts),
@@ -1357,6 +1844,21 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     *pos_out = plan.final_pos;
     return SRT_OK;
 }
+
+#ifdef RT_PROF
+// diagnostic build only: section counters of rt_device.h (64 words: 32 cycle sums, 32 counts)
+int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
+    if (!c || !out) return fail(SRT_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_prof), sizeof(unsigned long long) * 64));
+    if (reset) {
+        unsigned long long z[64] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rt_prof), z, sizeof(z)));
+    }
+    return SRT_OK;
+}
+#endif
 
 int srt_synchronize(srt_ctx* c) {
     if (!c) return fail(SRT_ERR_ARG, "null ctx");

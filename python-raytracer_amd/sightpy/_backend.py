@@ -44,6 +44,8 @@ def context():
         dev = int(os.environ.get("SIGHTPY_DEVICE", os.environ.get("LOCAL_RANK", "0"))) % n.value
         ctx = ctypes.c_void_p()
         N.check(lib, lib.srt_create(dev, ctypes.byref(ctx)))
+        if os.environ.get("SIGHTPY_FRAME_KERNEL") is not None:  # A/B switch: 0 = per-depth wavefront kernels
+            N.check(lib, lib.srt_set_option(ctx, b"frame_kernel", int(os.environ["SIGHTPY_FRAME_KERNEL"])))
         _STATE["ctx"] = ctx
         _STATE["device"] = dev
     return _STATE["lib"], _STATE["ctx"]

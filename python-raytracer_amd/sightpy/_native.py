@@ -133,6 +133,8 @@ class RenderArgs(ctypes.Structure):
         ("out_rgb", _p),
         ("out_srgb8", _p),
         ("out_hit_id", _p),
+        ("flags", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -182,7 +184,8 @@ class TraceArgs(ctypes.Structure):
 
 
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
-ABI_VERSION = 1  # SRT_ABI_VERSION of include/sightpy_rt.h
+RENDER_ASYNC = 1  # SRT_RENDER_ASYNC
+ABI_VERSION = 2  # SRT_ABI_VERSION of include/sightpy_rt.h
 
 SIGNATURES = {
     "srt_abi_version": (ctypes.c_int, []),
@@ -202,6 +205,8 @@ SIGNATURES = {
     "srt_device_free": (ctypes.c_int, [_p, _p]),
     "srt_memcpy": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64]),
     "srt_synchronize": (ctypes.c_int, [_p]),
+    "srt_render_finish": (ctypes.c_int, [_p, ctypes.POINTER(Stats)]),
+    "srt_stream": (ctypes.c_int, [_p, ctypes.POINTER(_p)]),
     "srt_last_error": (ctypes.c_char_p, []),
 }
 

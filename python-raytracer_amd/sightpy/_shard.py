@@ -35,24 +35,37 @@ def assemble_index(height, world, band=BAND):
     return idx
 
 
+class RowGather:
+    """Reusable all-gather of padded row tiles for one (height, world, tile shape, device): the
+    gathered buffer and the row-assembly index are allocated once, so each frame costs one RCCL
+    `all_gather_into_tensor` plus one on-device row permutation (`index_select`)."""
+
+    def __init__(self, height, world, rest, dtype, device, group=None, band=BAND):
+        import torch
+
+        self.height, self.world, self.group, self.band = int(height), int(world), group, band
+        self.maxrows = max_shard_rows(height, world, band)
+        self.full = torch.empty((world * self.maxrows,) + tuple(rest), dtype=dtype, device=device)
+        self.idx = torch.as_tensor(assemble_index(height, world, band), device=device)
+
+    def __call__(self, padded):
+        """`padded`: this rank's tile with `maxrows` rows (rows beyond its shard are ignored)."""
+        import torch.distributed as dist
+
+        if dist.get_backend(self.group) == "gloo":
+            dist.all_gather(list(self.full.chunk(self.world)), padded, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.full, padded, group=self.group)
+        return self.full.index_select(0, self.idx)
+
+
 def gather_rows(tile, height, world, group=None, band=BAND):
     """All-gather each rank's row tile and return the full image on every rank.
 
     `tile` is a torch tensor of shape (len(shard_rows(...)), ...) on the collective's device
     (cuda for nccl, cpu for gloo).  Tiles are padded to the largest shard so a single
     `all_gather_into_tensor` (one RCCL collective) moves the frame."""
-    import torch
-    import torch.distributed as dist
-
-    maxrows = max_shard_rows(height, world, band)
-    rest = tuple(tile.shape[1:])
-    padded = tile.new_zeros((maxrows,) + rest)
+    g = RowGather(height, world, tile.shape[1:], tile.dtype, tile.device, group, band)
+    padded = tile.new_zeros((g.maxrows,) + tuple(tile.shape[1:]))
     padded[: tile.shape[0]] = tile
-    full = tile.new_empty((world * maxrows,) + rest)
-    if dist.get_backend(group) == "gloo":
-        # gloo has no all_gather_into_tensor; gather into views of the same buffer
-        dist.all_gather(list(full.chunk(world)), padded, group=group)
-    else:
-        dist.all_gather_into_tensor(full, padded, group=group)
-    idx = torch.as_tensor(assemble_index(height, world, band), device=full.device)
-    return full.index_select(0, idx)
+    return g(padded)

@@ -3,9 +3,9 @@
 set -e
 cd "$(dirname "$0")/../python-raytracer_amd/csrc"
 mkdir -p ../../build/abl
-for f in ${ABL:-SHADOW POW TEX FB APPEND QSTORE NOSHADE}; do
+for f in ${ABL:-SHADOW POW TEX FB APPEND QSTORE NOSHADE PROF}; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -munsafe-fp-atomics \
-    -DRT_ABL_$f -o ../../build/abl/libsightpy_hip_$f.so rt_kernels.hip &
+    -DRT_ABL_$f $( [ $f = PROF ] && echo -DRT_PROF ) -o ../../build/abl/libsightpy_hip_$f.so rt_kernels.hip &
 done
 wait
 ls -la ../../build/abl

@@ -23,6 +23,7 @@ for step in "$@"; do
     tests) run tests 900 python3 -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench_sync) run bench_sync 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sync ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
@@ -37,6 +38,7 @@ for step in "$@"; do
             run bench_shard2 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 2 ;;
     latency) run prof_latency 300 rocprofv3 --kernel-trace -d gpurun_out/prof_latency -o lat --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --size 64x1 --spp 1
              run prof_shard8 300 rocprofv3 --kernel-trace -d gpurun_out/prof_shard8 -o s8 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --shard-of 8 ;;
+    rehearse) run rehearse_gloo2 300 env SIGHTPY_BENCH_DEVICE=0 SIGHTPY_BENCH_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
     rngdev) run bench_rngdev 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --rng device ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
