@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--occupancy", type=int, default=0, help="experiment: kernel variant with this waves/SIMD bound")
+    ap.add_argument("--option", action="append", default=[],
+                    help="experiment: srt_set_option KEY=VALUE before rendering (repeatable)")
     ap.add_argument("--sync", action="store_true",
                     help="one frame at a time (host waits for each frame) instead of pipelined frames")
     ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
@@ -143,6 +145,9 @@ def main():
     lib, ctx = B.context()
     if args.occupancy:
         N.check(lib, lib.srt_set_option(ctx, b"occupancy", args.occupancy))
+    for kv in args.option:
+        k, v = kv.split("=")
+        N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
     B.upload(sc)
     rows = shard_rows(H, world, rank) if world > 1 else np.arange(H)
     if args.shard_of > 1 and world == 1:

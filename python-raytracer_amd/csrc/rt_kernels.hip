@@ -86,7 +86,7 @@ struct TraceParams {
     int spp;           // samples of this pass (k_primary)
     int spt;           // samples per thread: k_primary item i = (pixel i % npix, samples [g*spt, g*spt+spt)),
                        // g = i / npix; spt < spp (small frames) adds to a zeroed framebuffer with atomics
-    int pad_;
+    int chain;         // k_trace: trace each ray's whole (single-child) chain in-thread, see k_trace
     int32_t* hit_out;  // [spp][npix] or null
     // frame kernel (k_frame): per-wave ray rings in HBM, slot s = rays [s * ring_cap, (s+1) * ring_cap)
     Queue ring;
@@ -375,15 +375,55 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
 
 // Depth d >= 1: blocks b, b + NSHARD, ... drain input shard b % NSHARD and append to output shard
 // b % NSHARD.
-template <uint32_t MATS, int OCC = 2>
+// Chain mode emitter (scenes whose rays have at most one child): the child replaces the ray in the
+// thread instead of going to the next depth's queue.  A second child (two colliders tied at the
+// same distance) has no place: it raises the retry flag and the host renders the frame again
+// without chain mode.
+struct ChainEmit {
+    const TraceParams& P;
+    const Ray& r;
+    uint32_t round;
+    uint32_t* shadow_acc;
+    Ray* next;
+    bool* has;
+
+    __device__ void local(d3 c) const { fb_add(P.fb, P.npix, r.pix, r.w, c); }
+    __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
+    __device__ void put(const Child& c, uint32_t path) const {
+        if (*has) {
+            P.flags[1] = 2u;
+            return;
+        }
+        *has = true;
+        next->o = c.o;
+        next->d = c.d;
+        next->w = mul(r.w, c.w);
+        next->pix = r.pix;
+        next->meta = pack_meta(c.medium, meta_depth(r.meta) + 1, c.dfl);
+        next->path = path;
+    }
+    __device__ void child(const Child& c) const { put(c, child_path(r.path, c.slot, round)); }
+    __device__ void diffuse(const DiffuseGen& g, int mi) const {
+        const auto& m = P.S.mat[mi];
+        for (int k = 0; k < g.count; ++k) {
+            Rng rng;
+            const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
+            rng.init(P.seed, r.pix, cpath, 0xD1000000u | meta_depth(r.meta));
+            put(diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
+        }
+    }
+};
+
+template <uint32_t MATS, int OCC = 2, bool CHAIN = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
     TraceParams P = P0;
-    stage_luts(P);
     const uint32_t shard = blockIdx.x % NSHARD;
-    uint32_t err = 0;
-    uint32_t shadow = 0;
     const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
     const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
+    if (blk * BLOCK >= n) return;  // nothing in this block's part of the shard (block-uniform)
+    stage_luts(P);
+    uint32_t err = 0;
+    uint32_t shadow = 0;
     const int64_t off = (int64_t)shard * P.seg;
     for (int64_t base = blk * BLOCK; base < n; base += nblk * BLOCK) {
         const int64_t i = base + threadIdx.x;
@@ -398,7 +438,28 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
         }
         RT_ACC(13, tq0);
         RT_T0(tt1);
-        trace_one<MATS>(P, r, active, err, nullptr, GpuEmit{P, r, shard, 0u, &shadow, nullptr});
+        if (!CHAIN) {
+            trace_one<MATS>(P, r, active, err, nullptr, GpuEmit{P, r, shard, 0u, &shadow, nullptr});
+        } else {
+            // the rest of each ray's path in this thread: lanes advance one depth per iteration, so
+            // the live lanes of an iteration share a depth (counted per wave into the shard's
+            // counter of that depth, as the queue appends would have)
+            bool live = active;
+            int d = P.depth;
+            for (;;) {
+                Ray nx = r;
+                bool has = false;
+                trace_one<MATS>(P, r, live, err, nullptr, ChainEmit{P, r, 0u, &shadow, &nx, &has});
+                live = live && has;
+                r = nx;
+                ++d;
+                const uint64_t m = __ballot(live);
+                if (m == 0) break;
+                if (live && lanes_below(m) == 0 && d < SRT_MAX_DEPTHS)  // the lowest live lane
+                    atomicAdd(P.cnt_out + (int64_t)(d - P.depth - 1) * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
+                if (d > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
+            }
+        }
         RT_ACC(14, tt1);
     }
     if (err) atomicOr(&P.flags[0], err);
@@ -626,21 +687,22 @@ struct Variant {
     void (*primary)(TraceParams);
     void (*trace)(TraceParams);
     void (*frame)(TraceParams);
+    void (*chain)(TraceParams);
 };
 // occupancy experiments for the headline scene (srt_set_option "occupancy" = 1 (index 2), 3, 4);
 // the default instantiations use 2 waves/SIMD, the fastest measured (profiles/)
 const Variant OCC_VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>, k_frame<MATS_GLOSSY_SKY, 1>},
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>, k_frame<MATS_GLOSSY_SKY, 3>},
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>, k_frame<MATS_GLOSSY_SKY, 4>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>, k_frame<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1, true>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>, k_frame<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3, true>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>, k_frame<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4, true>},
 };
 int g_occupancy = 0;
 const Variant VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>, k_frame<MATS_GLOSSY_SKY>},
-    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC>, k_frame<MATS_DIELECTRIC>},
-    {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>, k_frame<MATS_FILM>},
-    {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>, k_frame<MATS_MC>},
-    {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>, k_frame<MAT_ALL>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>, k_frame<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY, 2, true>},
+    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC>, k_frame<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC, 2, true>},
+    {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>, k_frame<MATS_FILM>, k_trace<MATS_FILM, 2, true>},
+    {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>, k_frame<MATS_MC>, k_trace<MATS_MC, 2, true>},
+    {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>, k_frame<MAT_ALL>, k_trace<MAT_ALL, 2, true>},
 };
 const Variant& pick_variant(uint32_t mats) {
     if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
@@ -918,6 +980,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
 // shape of one frame's passes (what the read-back of its counters needs)
 struct FramePlan {
     bool frame = false;  // rendered by k_frame (counts are totals, not queue fills)
+    int chain_from = 0;  // > 0: k_trace at this depth runs in chain mode and no deeper kernel is launched
     int64_t npix = 0;
     int spp = 0, batch = 0, npass = 0, dcap = 0, nev = 0;
     int64_t cnt_words = 0, pass_words = 0;
@@ -974,6 +1037,12 @@ struct srt_ctx {
     // ex1 1080p d5 13388 vs 10478, ex3 1080p d8 8950 vs 9585, ex4 4K d6 14081 vs 17494,
     // cornell 800x800 512 spp 3542 vs 4073.
     int use_frame = -1;
+    // chain mode of the wavefront path (single-child scenes): from the first depth >= 2 whose ray
+    // count in the previous frame of the same shape was below chain_rays
+    int64_t chain_rays = 600000;
+    bool chain_ok = true;  // cleared when a tie produced a second child in chain mode
+    int64_t hint_key[3] = {-1, -1, -1};
+    int64_t hint[SRT_MAX_DEPTHS] = {};
     Queue ring{};
     int64_t ring_cap = 0;
     int nslot = 0;
@@ -1142,6 +1211,7 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
         int rc;
         if ((rc = check_flags(hp[F.cnt_words]))) return rc;
         overflow |= hp[F.cnt_words + 1] != 0;
+        if (hp[F.cnt_words + 1] & 2u) c->chain_ok = false;  // a tie gave a chained ray two children
     }
     if (overflow) return SRT_RETRY_OVERFLOW;
     double ms_trace = 0.0, ms_primary = 0.0;
@@ -1174,6 +1244,9 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
     S.n_depths = F.dcap + 1;
     S.total_rays = 0;
     for (int d = 0; d <= F.dcap; ++d) S.total_rays += S.rays_per_depth[d];
+    // per-pass ray counts of this frame shape: the next frame's chain-mode plan
+    c->hint_key[0] = F.npix; c->hint_key[1] = F.spp; c->hint_key[2] = F.batch;
+    for (int d = 0; d < SRT_MAX_DEPTHS; ++d) c->hint[d] = S.rays_per_depth[d] / std::max(1, F.npass);
     return SRT_OK;
 }
 
@@ -1269,6 +1342,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
     if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
     if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
+    if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
     return fail(SRT_ERR_ARG, std::string("unknown option ") + key);
@@ -1355,6 +1429,8 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     c->fanout = fan;
     c->mats = 0;
     for (int i = 0; i < d->n_materials; ++i) c->mats |= mat_bit(d->materials[i].type);
+    c->chain_ok = true;
+    c->hint_key[0] = -1;  // ray counts of another scene are no plan for this one
     c->has_scene = true;
     return SRT_OK;
 }
@@ -1406,13 +1482,19 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     F.cnt_words = (int64_t)SRT_MAX_DEPTHS * NSHARD;
     F.pass_words = F.cnt_words + 2;
     F.frame = c->use_frame < 0 ? c->fanout > 1 : c->use_frame != 0;
+    if (!F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
+        c->hint_key[2] == batch) {
+        for (int d = 2; d <= F.dcap; ++d)
+            if (c->hint[d] < c->chain_rays) { F.chain_from = d; break; }
+    }
     // frames in flight use the buffers below: a synchronous frame, or one that would reallocate
     // anything, first waits for them (and reports their errors)
     if (c->async_pending > 0) {
         const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && a->n_rows <= c->cam_cap[2] &&
                           3 * npix <= c->fb_cap && 3 * npix <= c->rgb_cap && 3 * npix <= c->u8_cap &&
                           (int64_t)batch * npix * c->fanout <= c->seg * NSHARD && F.npass == c->async_plan.npass &&
-                          F.dcap == c->async_plan.dcap && F.frame == c->async_plan.frame;
+                          F.dcap == c->async_plan.dcap && F.frame == c->async_plan.frame &&
+                          F.chain_from == c->async_plan.chain_from;
         if (!async || !same)
             if ((rc = finish_async(c, nullptr))) return rc;
     }
@@ -1537,12 +1619,19 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             P.fb_first = 0;
             for (int d = 1; d <= F.dcap; ++d) {
+                if (F.chain_from > 0 && d > F.chain_from) {
+                    HIP_TRY(hipEventRecord(ev[1 + d], c->stream));  // traced by the chain kernel
+                    continue;
+                }
                 P.depth = d;
                 P.qin = c->q[d & 1];
                 P.qout = c->q[(d + 1) & 1];
                 P.cnt_in = c->counts + (int64_t)d * NSHARD;
                 P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-                hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream, P);
+                P.chain = (d == F.chain_from);
+                P.dcap = F.dcap;
+                hipLaunchKernelGGL(P.chain ? V.chain : V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream,
+                                   P);
                 HIP_TRY(hipGetLastError());
                 HIP_TRY(hipEventRecord(ev[1 + d], c->stream));
             }

@@ -192,3 +192,71 @@ def test_example3_1080p_d8_counts_match_reference_survey():
     out = _backend().render_scene(sc, 4, jitter=jit, seed=1)
     assert out.stats["rays_per_depth"] == [8294400, 4847603, 2862842, 2874155, 2799708, 2840696, 2741719,
                                            2752695, 2692499]
+
+
+def _set_option(key, value):
+    import ctypes
+
+    lib, ctx = _backend().context()
+    rc = lib.srt_set_option(ctx, key.encode(), ctypes.c_int64(value))
+    assert rc == 0, lib.srt_last_error()
+
+
+@pytest.mark.parametrize("name,builder,depth", DETERMINISTIC)
+@pytest.mark.parametrize("mode", ["wavefront", "wavefront+chain", "frame"])
+def test_gpu_every_kernel_path_matches_reference(name, builder, depth, mode):
+    """Every example through each trace strategy, whatever the automatic choice would be: the
+    per-depth wavefront kernels, the same with chain mode from depth 2 (the second render of a
+    shape; single-child scenes only), and the frame kernel."""
+    g = golden(name)
+    W, H, spp = int(g["width"]), int(g["height"]), int(g["spp"])
+    sc = builder(W, H, depth)
+    np.random.seed(int(g["seed"]))
+    jit = sc.camera.draw_jitter(spp)
+    _set_option("frame_kernel", 1 if mode == "frame" else 0)
+    _set_option("chain_rays", 1 << 40 if mode == "wavefront+chain" else 0)
+    try:
+        B = _backend()
+        for _ in range(2 if mode == "wavefront+chain" else 1):
+            out = B.render_scene(sc, spp, jitter=jit, seed=1, want_hits=True)
+    finally:
+        _set_option("frame_kernel", -1)
+        _set_option("chain_rays", 600000)
+    assert np.array_equal(out.hit_ids, g["hit_id"])
+    assert out.stats["rays_per_depth"][: len(g["depth_counts"])] == g["depth_counts"].tolist()
+    np.testing.assert_allclose(out.rgb, g["rgb"], rtol=RTOL, atol=ATOL)
+    _close_u8(out.srgb8, g["srgb8"])
+
+
+def test_gpu_async_frames_match_sync_frame():
+    """SRT_RENDER_ASYNC frames (pipelined, device outputs) equal a synchronous render."""
+    import ctypes
+    from sightpy import _native as N
+
+    B = _backend()
+    sc = scenes.example1(160, 120, 4)
+    np.random.seed(3)
+    jit = np.ascontiguousarray(sc.camera.draw_jitter(2))
+    ref = B.render_scene(sc, 2, jitter=jit, seed=5)
+    lib, ctx = B.context()
+    npix = 160 * 120
+    dj = B.device_buffer("test_jit", jit.nbytes)
+    N.check(lib, lib.srt_memcpy(ctx, dj, N.ptr(jit), jit.nbytes))
+    drgb = B.device_buffer("test_rgb", 3 * npix * 8)
+    du8 = B.device_buffer("test_u8", 3 * npix)
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, 120, 0
+    a.jitter, a.seed, a.out_rgb, a.out_srgb8, a.out_hit_id = dj, 5, drgb, du8, None
+    a.flags = N.RENDER_ASYNC
+    cd = B.camera_desc(sc.camera)
+    st = N.Stats()
+    for _ in range(4):
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+    N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(st)))
+    rgb = np.empty((3, npix))
+    u8 = np.empty((npix, 3), dtype=np.uint8)
+    N.check(lib, lib.srt_memcpy(ctx, N.ptr(rgb), drgb, rgb.nbytes))
+    N.check(lib, lib.srt_memcpy(ctx, N.ptr(u8), du8, u8.nbytes))
+    assert st.as_dict()["total_rays"] == ref.stats["total_rays"]
+    np.testing.assert_allclose(rgb, ref.rgb, rtol=1e-12, atol=1e-15)
+    assert np.array_equal(u8.reshape(120, 160, 3), ref.srgb8)

@@ -1,5 +1,5 @@
-for fk in 1 0; do
-  for c in example1_1080p_d5 example3_1080p_d8 example4_4k_d6 cornell_800_s512; do
-    SIGHTPY_FRAME_KERNEL=$fk timeout -k 10 300 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_${c}_fk$fk.log 2>&1 || exit 1
-  done
+bash tools/gpu_session.sh smoke tests || exit 1
+for cr in 0 200000 600000 1500000; do
+  timeout -k 10 120 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --option chain_rays=$cr > gpurun_out/chain_$cr.log 2>&1 || exit 1
+  timeout -k 10 120 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --option chain_rays=$cr --shard-of 8 > gpurun_out/chain8_$cr.log 2>&1 || exit 1
 done
