@@ -69,7 +69,7 @@ def cpu_baseline(builder, W, H, depth, spp, budget_s=20.0):
             "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
 
 
-def pmc_traffic(config):
+def pmc_traffic(config, kernel="k_primary"):
     """HBM bytes per k_primary launch from the newest committed PMC summary of this config
     (profiles/rNN_traffic_<config>.json, written by tools/pmc_traffic.py from two separate
     rocprofv3 --pmc passes of this same bench command), or None."""
@@ -78,7 +78,7 @@ def pmc_traffic(config):
         return None, None
     rec = json.loads(files[-1].read_text())
     for name, k in rec["kernels"].items():
-        if "k_primary" in name and "traffic_bytes" in k:
+        if kernel in name and "traffic_bytes" in k:
             return k["traffic_bytes"] / 1e9, files[-1].name
     return None, None
 
@@ -278,9 +278,15 @@ def main():
     prim_ms = np.mean([s["ms_primary_kernel"] for s in stats])
     trace_ms = np.mean([s["ms_trace_kernels"] for s in stats])
     rpd = stats[0]["rays_per_depth"]
-    achieved = rpd[0] * BYTES_PER_RAY / (prim_ms * 1e-3) / 1e9
+    frame_path = stats[0]["kernel_path"] == "frame"
+    # the dominant kernel: k_primary (depth 0) on the wavefront path; k_frame (every ray of the
+    # pass) on the frame-kernel path used for branching scenes
+    prim_rays = stats[0]["total_rays"] if frame_path else rpd[0]
+    achieved = prim_rays * BYTES_PER_RAY / (prim_ms * 1e-3) / 1e9
     family = stats[0]["total_rays"] * BYTES_PER_RAY / (trace_ms * 1e-3) / 1e9
-    traffic_gb, traffic_src = pmc_traffic(args.config)
+    # (PMC summaries are per launch of the full configuration: none for diagnostic shapes)
+    traffic_gb, traffic_src = (None, None) if (args.shard_of or args.size or args.spp) else \
+        pmc_traffic(args.config, "k_frame" if frame_path else "k_primary")
     if rank == 0:
         rec = {
             "metric": "Mrays/sec (primary+secondary) at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
@@ -298,16 +304,19 @@ def main():
             "data": "synthetic: %s; jitter = reference numpy stream seed 0 (%s)" % (label, args.rng),
             "config": {"workload": label, "width": W, "height": H, "max_ray_depth": depth, "spp": spp,
                        "rays_per_frame": int(total_rays), "rays_per_depth_rank0": rpd,
-                       "shadow_rays_rank0": stats[0]["shadow_rays"], "parallelism": ("row-band shards x%d" % world) if not args.shard_of
+                       "shadow_rays_rank0": stats[0]["shadow_rays"], "kernel_path": stats[0]["kernel_path"],
+                       "chain_from_depth": stats[0]["chain_from"], "parallelism": ("row-band shards x%d" % world) if not args.shard_of
                        else "diagnostic: rank 0 of %d row-band shards, no gather" % args.shard_of,
                        "frame_ms": round(ms_step, 4)},
-            "roofline": {"bound": "hbm", "kernel": "k_primary (depth 0: raygen + nearest hit + shading, fused)",
+            "roofline": {"bound": "hbm",
+                         "kernel": "k_frame (whole pass: every ray of every depth, one wave per 64-pixel tile)"
+                         if frame_path else "k_primary (depth 0: raygen + nearest hit + shading, fused)",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic_gb is None else round(traffic_gb, 4),
                          "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "algorithmic_GB_per_launch": round(rpd[0] * BYTES_PER_RAY / 1e9, 4),
+                         "algorithmic_GB_per_launch": round(prim_rays * BYTES_PER_RAY / 1e9, 4),
                          "bytes_per_ray": BYTES_PER_RAY, "kernel_ms": round(float(prim_ms), 4),
                          "all_trace_kernels": {"ms": round(float(trace_ms), 4), "achieved_GBs": round(family, 2),
                                                "frac": round(family / HBM_PEAK_GBS, 4)}},

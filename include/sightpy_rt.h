@@ -220,6 +220,9 @@ typedef struct srt_stats {
     double ms_trace_kernels; /* sum of trace-kernel durations, HIP events */
     double ms_primary_kernel;
     int64_t retries;         /* passes re-run after a queue overflow */
+    int32_t kernel_path;     /* 0: per-depth wavefront kernels (ms_primary_kernel = k_primary),
+                                1: frame kernel (ms_primary_kernel = k_frame, the whole pass) */
+    int32_t chain_from;      /* > 0: depths >= chain_from traced in chain mode by one k_trace */
 } srt_stats;
 
 typedef struct srt_trace_args {

@@ -727,7 +727,20 @@ __global__ __launch_bounds__(BLOCK) void k_pass_end(uint32_t* counts, int64_t wo
 }
 
 __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npix, unsigned long long* shadow,
-                                                  uint32_t* shadow_host, double spp, double* rgb, uint8_t* u8) {
+                                                  uint32_t* shadow_host, double spp, double* rgb, uint8_t* u8,
+                                                  uint32_t* counts, int64_t words, uint32_t* flags, uint32_t* host,
+                                                  uint32_t* host_flags) {
+    // block 0 also ends the last pass (the work of k_pass_end, one launch less per frame)
+    if (blockIdx.x == 0 && words > 0) {
+        for (int64_t i = threadIdx.x; i < words; i += BLOCK) {
+            host[i] = counts[i];
+            counts[i] = 0u;
+        }
+        if (threadIdx.x < 2) {
+            host_flags[threadIdx.x] |= flags[threadIdx.x];
+            flags[threadIdx.x] = 0u;
+        }
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // the frame's shadow-ray count (NSHARD counters) to the host, zeroed for the next frame (no
         // kernel of this frame adds to them any more)
@@ -1039,7 +1052,7 @@ struct srt_ctx {
     int use_frame = -1;
     // chain mode of the wavefront path (single-child scenes): from the first depth >= 2 whose ray
     // count in the previous frame of the same shape was below chain_rays
-    int64_t chain_rays = 600000;
+    int64_t chain_rays = 1000000;
     bool chain_ok = true;  // cleared when a tie produced a second child in chain mode
     int64_t hint_key[3] = {-1, -1, -1};
     int64_t hint[SRT_MAX_DEPTHS] = {};
@@ -1232,7 +1245,7 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
         float ms;
         HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
         ms_primary += ms;
-        HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[F.dcap + 1]));
+        HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[F.chain_from > 0 ? F.chain_from + 1 : F.dcap + 1]));
         ms_trace += ms;
     }
     const uint32_t* hshadow = c->host + F.npass * F.pass_words;
@@ -1242,6 +1255,8 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
     S.ms_device = ms_trace;
     S.shadow_rays = (int64_t)(hshadow[0] | (uint64_t)hshadow[1] << 32);
     S.n_depths = F.dcap + 1;
+    S.kernel_path = F.frame ? 1 : 0;
+    S.chain_from = F.chain_from;
     S.total_rays = 0;
     for (int d = 0; d <= F.dcap; ++d) S.total_rays += S.rays_per_depth[d];
     // per-pass ray counts of this frame shape: the next frame's chain-mode plan
@@ -1484,7 +1499,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     F.frame = c->use_frame < 0 ? c->fanout > 1 : c->use_frame != 0;
     if (!F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
         c->hint_key[2] == batch) {
-        for (int d = 2; d <= F.dcap; ++d)
+        for (int d = 1; d <= F.dcap; ++d)
             if (c->hint[d] < c->chain_rays) { F.chain_from = d; break; }
     }
     // frames in flight use the buffers below: a synchronous frame, or one that would reallocate
@@ -1619,10 +1634,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             HIP_TRY(hipEventRecord(ev[1], c->stream));
             P.fb_first = 0;
             for (int d = 1; d <= F.dcap; ++d) {
-                if (F.chain_from > 0 && d > F.chain_from) {
-                    HIP_TRY(hipEventRecord(ev[1 + d], c->stream));  // traced by the chain kernel
-                    continue;
-                }
+                if (F.chain_from > 0 && d > F.chain_from) break;  // traced by the chain kernel
                 P.depth = d;
                 P.qin = c->q[d & 1];
                 P.qout = c->q[(d + 1) & 1];
@@ -1638,10 +1650,13 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             }
             uint32_t* hp = c->host + p * F.pass_words;
             // counters of this pass -> pinned host words [0, used_words) (the unused depths are zero
-            // on the host), flags OR-ed into the two words at [cnt_words, cnt_words + 2)
-            hipLaunchKernelGGL(k_pass_end, dim3(1), dim3(BLOCK), 0, c->stream, c->counts, used_words, c->flags,
-                               hp, hp + F.cnt_words);
-            HIP_TRY(hipGetLastError());
+            // on the host), flags OR-ed into the two words at [cnt_words, cnt_words + 2); the last
+            // pass's are handed over by k_resolve
+            if (p + 1 < F.npass) {
+                hipLaunchKernelGGL(k_pass_end, dim3(1), dim3(BLOCK), 0, c->stream, c->counts, used_words, c->flags,
+                                   hp, hp + F.cnt_words);
+                HIP_TRY(hipGetLastError());
+            }
             if (a->out_hit_id && !hit_dev)
                 HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->hit, (size_t)nrays * 4,
                                        hipMemcpyDeviceToHost, c->stream));
@@ -1649,8 +1664,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         uint32_t* hshadow = c->host + F.npass * F.pass_words;
         // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
         const bool fused = F.frame && F.npass == 1;
+        uint32_t* hlast = c->host + (F.npass - 1) * F.pass_words;
         hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb,
-                           fused ? (int64_t)0 : npix, c->shadow, hshadow, (double)a->spp, res_rgb, res_u8);
+                           fused ? (int64_t)0 : npix, c->shadow, hshadow, (double)a->spp, res_rgb, res_u8, c->counts,
+                           used_words, c->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
         c->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
         if (async) {

@@ -150,6 +150,8 @@ class Stats(ctypes.Structure):
         ("ms_trace_kernels", ctypes.c_double),
         ("ms_primary_kernel", ctypes.c_double),
         ("retries", ctypes.c_int64),
+        ("kernel_path", ctypes.c_int32),
+        ("chain_from", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -167,6 +169,8 @@ class Stats(ctypes.Structure):
             "ms_trace_kernels": float(self.ms_trace_kernels),
             "ms_primary_kernel": float(self.ms_primary_kernel),
             "retries": int(self.retries),
+            "kernel_path": "frame" if int(self.kernel_path) == 1 else "wavefront",
+            "chain_from": int(self.chain_from),
         }
 
 

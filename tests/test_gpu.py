@@ -221,7 +221,7 @@ def test_gpu_every_kernel_path_matches_reference(name, builder, depth, mode):
             out = B.render_scene(sc, spp, jitter=jit, seed=1, want_hits=True)
     finally:
         _set_option("frame_kernel", -1)
-        _set_option("chain_rays", 600000)
+        _set_option("chain_rays", 1000000)
     assert np.array_equal(out.hit_ids, g["hit_id"])
     assert out.stats["rays_per_depth"][: len(g["depth_counts"])] == g["depth_counts"].tolist()
     np.testing.assert_allclose(out.rgb, g["rgb"], rtol=RTOL, atol=ATOL)

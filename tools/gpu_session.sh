@@ -25,8 +25,8 @@ for step in "$@"; do
     bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench_sync) run bench_sync 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sync ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_write) run pmc_write_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
     configs) for c in example3_1080p_d8 example4_4k_d6 cornell_800_s512; do run "bench_$c" 600 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline; done ;;
     occ) for o in 0 2 3 4; do run "bench_occ$o" 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --occupancy $o; done ;;
     abl) for f in build/abl/libsightpy_hip_*.so; do n=$(basename $f .so); run "abl_${n#libsightpy_hip_}" 300 env SIGHTPY_HIP_LIB=$f python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline; done ;;
