@@ -1,0 +1,178 @@
+// rt_bvh.h -- host-side BVH build over the Triangle colliders of a scene (TriangleMesh,
+// the reference's own TODO, `sightpy/geometry/triangle_mesh.py:7-9`).
+//
+// Used by srt_upload_scene (rt_kernels.hip) and by the CPU check harness (rt_hostcheck.cpp), so the
+// traversal in rt_device.h (bvh_nearest / bvh_shadow) is tested on both sides.  The BVH is only an
+// accelerator: nearest_hit merges its triangles with the reference's order-independent rule
+// (smallest distance, then lowest collider index, ties recorded), so results equal the linear loop
+// over `scene.collider_list` (ray.py:124-132).
+//
+// Build: binned SAH (16 bins on the longest centroid axis), leaves of at most 4 triangles, depth
+// capped below the traversal stack.  Boxes are the triangles' vertex boxes inflated by
+// 1e-9 * (1 + max |coordinate|): the reference intersects the plane through the centroid and tests
+// edge half-spaces with >= 0, so a hit point may sit a few ulps outside the vertex box.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "rt_device.h"
+
+namespace rt {
+
+constexpr int BVH_MIN_TRIANGLES = 8;  // fewer triangles stay in the linear collider loop
+constexpr int BVH_LEAF = 4;
+constexpr int BVH_MAX_DEPTH = BVH_STACK - 4;
+
+struct BvhBuild {
+    std::vector<BvhNode> nodes;
+    std::vector<int32_t> tri;  // collider index per leaf slot
+    std::vector<int32_t> lin;  // colliders outside the BVH, ascending
+};
+
+namespace bvh_detail {
+struct Item {
+    double lo[3], hi[3], c[3];
+    int32_t col;
+};
+inline void grow(double* lo, double* hi, const double* plo, const double* phi) {
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = std::min(lo[k], plo[k]);
+        hi[k] = std::max(hi[k], phi[k]);
+    }
+}
+inline double area(const double* lo, const double* hi) {
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (!(dx >= 0.0)) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+}  // namespace bvh_detail
+
+inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
+    using namespace bvh_detail;
+    out.nodes.clear();
+    out.tri.clear();
+    out.lin.clear();
+    std::vector<Item> items;
+    for (int i = 0; i < n; ++i)
+        if (col[i].type == SRT_TRIANGLE) {
+            Item it;
+            const double* p = col[i].p;  // p1 = p[6..8], p2 = p[9..11], p3 = p[12..14]
+            double m = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                it.lo[k] = std::min(std::min(p[6 + k], p[9 + k]), p[12 + k]);
+                it.hi[k] = std::max(std::max(p[6 + k], p[9 + k]), p[12 + k]);
+                m = std::max(m, std::max(std::fabs(it.lo[k]), std::fabs(it.hi[k])));
+            }
+            const double eps = 1e-9 * (1.0 + m);
+            for (int k = 0; k < 3; ++k) {
+                it.lo[k] -= eps;
+                it.hi[k] += eps;
+                it.c[k] = 0.5 * (it.lo[k] + it.hi[k]);
+            }
+            it.col = i;
+            items.push_back(it);
+        }
+    if ((int)items.size() < BVH_MIN_TRIANGLES) {
+        for (int i = 0; i < n; ++i) out.lin.push_back(i);
+        return;
+    }
+    for (int i = 0; i < n; ++i)
+        if (col[i].type != SRT_TRIANGLE) out.lin.push_back(i);
+
+    struct Task {
+        int node, begin, end, depth;
+    };
+    out.nodes.push_back(BvhNode{});
+    std::vector<Task> tasks{{0, 0, (int)items.size(), 0}};
+    while (!tasks.empty()) {
+        const Task t = tasks.back();
+        tasks.pop_back();
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = t.begin; i < t.end; ++i) {
+            grow(lo, hi, items[i].lo, items[i].hi);
+            grow(clo, chi, items[i].c, items[i].c);
+        }
+        BvhNode& nd = out.nodes[t.node];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[k] = lo[k];
+            nd.hi[k] = hi[k];
+        }
+        const int cnt = t.end - t.begin;
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        const double ext = chi[axis] - clo[axis];
+        int mid = -1;
+        if (cnt > BVH_LEAF && t.depth < BVH_MAX_DEPTH && ext > 0.0) {
+            // binned SAH on the longest centroid axis
+            constexpr int NB = 16;
+            double blo[NB][3], bhi[NB][3];
+            int bc[NB] = {};
+            for (int b = 0; b < NB; ++b)
+                for (int k = 0; k < 3; ++k) {
+                    blo[b][k] = INFINITY;
+                    bhi[b][k] = -INFINITY;
+                }
+            auto bin_of = [&](const Item& it) {
+                int b = (int)((it.c[axis] - clo[axis]) / ext * NB);
+                return std::min(NB - 1, std::max(0, b));
+            };
+            for (int i = t.begin; i < t.end; ++i) {
+                const int b = bin_of(items[i]);
+                bc[b]++;
+                grow(blo[b], bhi[b], items[i].lo, items[i].hi);
+            }
+            double best = INFINITY;
+            int best_split = -1;
+            for (int s = 1; s < NB; ++s) {
+                double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                double rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                int nl = 0, nr = 0;
+                for (int b = 0; b < s; ++b) {
+                    nl += bc[b];
+                    if (bc[b]) grow(llo, lhi, blo[b], bhi[b]);
+                }
+                for (int b = s; b < NB; ++b) {
+                    nr += bc[b];
+                    if (bc[b]) grow(rlo, rhi, blo[b], bhi[b]);
+                }
+                if (!nl || !nr) continue;
+                const double cost = nl * area(llo, lhi) + nr * area(rlo, rhi);
+                if (cost < best) {
+                    best = cost;
+                    best_split = s;
+                }
+            }
+            if (best_split > 0) {
+                auto it = std::partition(items.begin() + t.begin, items.begin() + t.end,
+                                         [&](const Item& x) { return bin_of(x) < best_split; });
+                mid = (int)(it - items.begin());
+            } else {
+                // every centroid in one bin: median split
+                mid = t.begin + cnt / 2;
+                std::nth_element(items.begin() + t.begin, items.begin() + mid, items.begin() + t.end,
+                                 [&](const Item& a, const Item& b) { return a.c[axis] < b.c[axis]; });
+            }
+            if (mid <= t.begin || mid >= t.end) mid = -1;
+        }
+        if (mid < 0) {
+            // leaf (also when too deep: larger leaves keep the traversal stack bounded)
+            nd.first = (int32_t)out.tri.size();
+            nd.count = cnt;
+            for (int i = t.begin; i < t.end; ++i) out.tri.push_back(items[i].col);
+            continue;
+        }
+        const int left = (int)out.nodes.size();
+        nd.first = left;
+        nd.count = 0;
+        out.nodes.push_back(BvhNode{});
+        out.nodes.push_back(BvhNode{});
+        tasks.push_back({left, t.begin, mid, t.depth + 1});
+        tasks.push_back({left + 1, mid, t.end, t.depth + 1});
+    }
+}
+
+}  // namespace rt

@@ -221,9 +221,25 @@ struct SceneView {
         uint64_t lut_lds_bits_;
     };
     int nlut_lds;
+    // Triangle colliders of large meshes live in a BVH (rt_bvh.h); `lin` lists the colliders
+    // intersected one by one (ascending; every collider when there is no BVH)
+    int nlin;
+    const RT_RO int32_t* lin;
+    const RT_RO struct BvhNode* bvh;
+    const RT_RO int32_t* bvh_tri;  // collider index of each BVH leaf slot
+    int bvh_nodes;                 // 0: no BVH
+    int pad_;
 };
 // the host builds SceneView/TraceParams and the device reads them: the layout must agree
-static_assert(sizeof(SceneView) == 144 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
+static_assert(sizeof(SceneView) == 176 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
+
+// BVH node (56 B): box [lo, hi] (inflated so that rounding never excludes a triangle's hit point);
+// count > 0: leaf of bvh_tri[first, first + count); count == 0: children at first and first + 1
+struct BvhNode {
+    double lo[3], hi[3];
+    int32_t first, count;
+};
+constexpr int BVH_STACK = 64;
 
 // lut[b] of texture `tid` (LDS copy when staged)
 RT_HD double tex_lut(const SceneView& S, int tid, uint8_t b) {
@@ -528,13 +544,92 @@ RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double
 // Nearest collider over the scene (ray.py:124-132): nearest = reduce(np.minimum, distances);
 // a collider is hit where nearest != FARAWAY and its distance == nearest.  Returns the first
 // such collider (-1 if none); `ties` reports that a later collider hit at the same distance.
+// Ray/box slab test: entry distance `tnear`; an axis whose slab product is NaN (an axis-parallel
+// ray exactly on a slab plane) constrains nothing (conservative).
+RT_HD bool box_hit(const RT_RO BvhNode& nd, d3 O, d3 inv, double& tnear) {
+    double t0 = -INFINITY, t1 = INFINITY;
+    const double o[3] = {O.x, O.y, O.z}, iv[3] = {inv.x, inv.y, inv.z};
+    for (int k = 0; k < 3; ++k) {
+        const double a = (nd.lo[k] - o[k]) * iv[k], b = (nd.hi[k] - o[k]) * iv[k];
+        if (a != a || b != b) continue;
+        t0 = fmax(t0, fmin(a, b));
+        t1 = fmin(t1, fmax(a, b));
+    }
+    tnear = t0;
+    return t0 <= t1 && t1 >= 0.0;
+}
+
+// Nearest BVH triangle, merged into (best, id, bo, ties) with the reference's rule independent of
+// visiting order: the smallest distance wins, among equal distances the lowest collider index,
+// and `ties` records that another collider hit at that distance.  Boxes entered beyond `best` are
+// pruned (a box entered exactly at `best` is still visited: it may hold a tie).  Triangles never
+// return NaN (a NaN ray fails every comparison of triangle_hit and misses).
+RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
+    const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
+    int stack[BVH_STACK];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const RT_RO BvhNode& nd = S.bvh[stack[--sp]];
+        double tn;
+        if (!box_hit(nd, O, inv, tn) || tn > best) continue;
+        if (nd.count > 0) {
+            for (int k = nd.first; k < nd.first + nd.count; ++k) {
+                const int c = S.bvh_tri[k];
+                double o;
+                const double t = triangle_hit(S.col[c].p, O, D, o);
+                if (t < best) { best = t; id = c; bo = o; ties = false; }
+                else if (t == best && best != FARAWAY) {
+                    ties = true;
+                    if (c < id) { id = c; bo = o; }
+                }
+            }
+        } else if (sp + 2 <= BVH_STACK) {
+            stack[sp++] = nd.first + 1;
+            stack[sp++] = nd.first;
+        }
+    }
+}
+
+// Any shadowed BVH triangle closer than `stop` along L: returns its distance, else FARAWAY.
+RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
+    const d3 inv = d3{1.0 / L.x, 1.0 / L.y, 1.0 / L.z};
+    int stack[BVH_STACK];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const RT_RO BvhNode& nd = S.bvh[stack[--sp]];
+        double tn;
+        if (!box_hit(nd, O, inv, tn) || tn >= stop) continue;
+        if (nd.count > 0) {
+            for (int k = nd.first; k < nd.first + nd.count; ++k) {
+                const RT_RO srt_collider& cc = S.col[S.bvh_tri[k]];
+                if (!(cc.flags & SRT_CF_SHADOW)) continue;
+                double o;
+                const double t = triangle_hit(cc.p, O, L, o);
+                if (t < stop) return t;
+            }
+        } else if (sp + 2 <= BVH_STACK) {
+            stack[sp++] = nd.first + 1;
+            stack[sp++] = nd.first;
+        }
+    }
+    return FARAWAY;
+}
+
+// BVH: compile the mesh traversal in (kernels instantiated for scenes without a BVH leave it out:
+// its stack would otherwise cost scratch and registers in every kernel)
+template <bool BVH = true>
 RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bool& ties) {
     double best = FARAWAY;
     int id = -1;
     double bo = FARAWAY;
     ties = false;
     bool nan = false;
-    for (int c = 0; c < S.ncol; ++c) {
+    // without a BVH `lin` is the identity: the loop then indexes the collider table directly
+    const int nl = BVH ? S.nlin : S.ncol;
+    for (int li = 0; li < nl; ++li) {
+        const int c = BVH ? S.lin[li] : li;
         double o;
         const RT_RO srt_collider& cc = S.col[c];
         if (cc.type == SRT_CUBOID && cc.p[42] != 0.0 && id >= 0) {
@@ -552,6 +647,7 @@ RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bo
         if (t < best) { best = t; id = c; bo = o; ties = false; }
         else if (t == best && id >= 0) ties = true;
     }
+    if (BVH && S.bvh_nodes > 0) bvh_nearest(S, O, D, best, id, bo, ties);
     if (nan || best == FARAWAY) { tn = nan ? NAN : FARAWAY; on = FARAWAY; ties = false; return -1; }
     tn = best;
     on = bo;
@@ -607,10 +703,15 @@ RT_HD Child mkchild(d3 o, d3 d, d3 w, uint32_t medium, uint32_t dfl, uint32_t sl
 }
 
 // min over the shadowed colliders of the distance along the light direction (glossy.py:53-59)
-RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L) {
+// `stop`: the caller only asks whether the result is >= stop (seelight), so the BVH pass may stop
+// at the first shadowing triangle closer than that
+template <bool BVH = true>
+RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L, double stop) {
     double best = FARAWAY;
     bool first = true;
-    for (int c = 0; c < S.ncol; ++c) {
+    const int nl = BVH ? S.nlin : S.ncol;
+    for (int li = 0; li < nl; ++li) {
+        const int c = BVH ? S.lin[li] : li;
         const RT_RO srt_collider& cc = S.col[c];
         if (!(cc.flags & SRT_CF_SHADOW)) continue;
         double o, t;
@@ -621,11 +722,12 @@ RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L) {
         best = first ? t : np_min(best, t);
         first = false;
     }
+    if (BVH && S.bvh_nodes > 0 && best >= stop) best = np_min(best, bvh_shadow(S, O, L, stop));
     return best;
 }
 
 // Glossy.get_color (glossy.py:25-110)
-template <class E>
+template <bool BVH = true, class E>
 RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, double orient,
                         E& em, uint32_t& err) {
     const RT_RO srt_material& m = S.mat[mi];
@@ -669,7 +771,7 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
         if (S.nshadow > 0) {
 #endif
             RT_T0(ts0);
-            double ln = shadow_nearest(S, l, nudged, L);
+            double ln = shadow_nearest<BVH>(S, l, nudged, L, dist);
             RT_ACC(5, ts0);
             seelight = (ln >= dist) ? 1.0 : 0.0;
             em.shadow(1);
@@ -937,6 +1039,8 @@ RT_HD Child diffuse_child(const SceneView& S, const RT_RO srt_material& m, const
 
 // Material-type bit masks: a kernel instantiated for MATS contains only those shading paths.
 constexpr uint32_t MAT_ALL = 0x3Fu;
+// not a material: the scene has a triangle BVH (kernels without this bit carry no traversal code)
+constexpr uint32_t MAT_BVH = 0x40u;
 constexpr uint32_t mat_bit(int type) { return 1u << type; }
 
 // Shade one (ray, collider) hit with a per-lane (possibly divergent) material.
@@ -946,7 +1050,7 @@ RT_HD void shade_hit(const SceneView& S, int cid, int mi, const Ray& r, double t
     const RT_RO srt_collider& c = S.col[cid];
     switch (S.mat[mi].type) {
         case SRT_GLOSSY:
-            if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy(S, c, mi, r, t, orient, em, err);
+            if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<(MATS & MAT_BVH) != 0>(S, c, mi, r, t, orient, em, err);
             break;
         case SRT_REFRACTIVE:
             if (MATS & mat_bit(SRT_REFRACTIVE)) shade_refractive(S, c, mi, r, t, orient, em, err, mc_u);

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_mt.h"
 
@@ -25,8 +26,22 @@ struct Scene {
     int has_diffuse = 0;
 };
 
+thread_local BvhBuild g_bvh;  // the BVH of the scene of the current call
+thread_local int g_use_bvh = 1;
+
 SceneView view_of(const srt_scene_desc* d) {
     SceneView S{};
+    if (g_use_bvh) {
+        bvh_build(d->colliders, d->n_colliders, g_bvh);
+    } else {
+        g_bvh = BvhBuild{};
+        for (int i = 0; i < d->n_colliders; ++i) g_bvh.lin.push_back(i);
+    }
+    S.nlin = (int)g_bvh.lin.size();
+    S.lin = g_bvh.lin.data();
+    S.bvh = g_bvh.nodes.empty() ? nullptr : g_bvh.nodes.data();
+    S.bvh_tri = g_bvh.tri.empty() ? nullptr : g_bvh.tri.data();
+    S.bvh_nodes = (int)g_bvh.nodes.size();
     S.col = d->colliders; S.mat = d->materials; S.tex = d->textures; S.texels = d->texels;
     S.lights = d->lights; S.media = d->media; S.glossy_f0 = d->glossy_f0; S.light_local = d->light_local;
     S.importance = d->importance;
@@ -98,14 +113,15 @@ void trace_one(const SceneView& S, const Ray& r, int depth, uint64_t seed, std::
     if (hit_slot) *hit_slot = id;
     if (id < 0) return;
     HostEmit em{S, r, next, fb, npix, seed, depth, 0u, &shadow};
-    shade_hit(S, id, S.col[id].material, r, t, o, em, err, mc_uniform(S, seed, depth, r, id, 0));
+    shade_hit<MAT_ALL | MAT_BVH>(S, id, S.col[id].material, r, t, o, em, err, mc_uniform(S, seed, depth, r, id, 0));
     if (ties) {
         uint32_t round = 1;
         for (int c = id + 1; c < S.ncol; ++c) {
             double oc;
             if (collider_hit(S.col[c], r.o, r.d, oc) == t) {
                 HostEmit et{S, r, next, fb, npix, seed, depth, round, &shadow};
-                shade_hit(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(S, seed, depth, r, c, round));
+                shade_hit<MAT_ALL | MAT_BVH>(S, c, S.col[c].material, r, t, oc, et, err,
+                                             mc_uniform(S, seed, depth, r, c, round));
                 ++round;
             }
         }
@@ -123,6 +139,14 @@ int err_code(uint32_t e) {
 extern "C" {
 
 const char* hc_last_error(void) { return g_err.c_str(); }
+
+// 1: triangle colliders of large meshes go through the BVH (as on the GPU); 0: linear loop only
+void hc_set_bvh(int on) { g_use_bvh = on; }
+int hc_bvh_nodes(const srt_scene_desc* d) {
+    BvhBuild b;
+    bvh_build(d->colliders, d->n_colliders, b);
+    return (int)b.nodes.size();
+}
 
 // Breadth-first render of `args->spp` samples (host pointers only); out_rgb = linear RGB / spp.
 int hc_render(const srt_scene_desc* d, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {

@@ -26,6 +26,7 @@
 #include <string>
 #include <vector>
 
+#include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_mt.h"
 
@@ -55,7 +56,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 752;
+constexpr size_t TRACE_PARAMS_BYTES = 784;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 
 struct Queue {
@@ -238,7 +239,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     bool ties = false;
     int id = -1;
     RT_T0(tn0);
-    if (active) id = nearest_hit(S, r.o, r.d, t, o, ties);
+    if (active) id = nearest_hit<(MATS & MAT_BVH) != 0>(S, r.o, r.d, t, o, ties);
     RT_ACC(1, tn0);
     if (hit_slot && active) *hit_slot = id;
     const Em& em = em0;
@@ -265,7 +266,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
             const int m = c.material;
             switch (S.mat[m].type) {
                 case SRT_GLOSSY:
-                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy(S, c, m, r, t, o, em, err);
+                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<(MATS & MAT_BVH) != 0>(S, c, m, r, t, o, em, err);
                     break;
                 case SRT_REFRACTIVE:
                     if (MATS & mat_bit(SRT_REFRACTIVE))
@@ -703,6 +704,9 @@ const Variant VARIANTS[] = {
     {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>, k_frame<MATS_FILM>, k_trace<MATS_FILM, 2, true>},
     {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>, k_frame<MATS_MC>, k_trace<MATS_MC, 2, true>},
     {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>, k_frame<MAT_ALL>, k_trace<MAT_ALL, 2, true>},
+    // scenes with a triangle BVH (TriangleMesh)
+    {MAT_ALL | MAT_BVH, k_primary<MAT_ALL | MAT_BVH>, k_trace<MAT_ALL | MAT_BVH>, k_frame<MAT_ALL | MAT_BVH>,
+     k_trace<MAT_ALL | MAT_BVH, 2, true>},
 };
 const Variant& pick_variant(uint32_t mats) {
     if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
@@ -1427,6 +1431,21 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     S.ncol = d->n_colliders; S.nmat = d->n_materials; S.ntex = d->n_textures; S.nlights = d->n_lights;
     S.nmedia = d->n_media; S.nimp = d->n_importance;
     S.nshadow = 0;
+    {
+        // triangle meshes: BVH over the Triangle colliders, the rest intersected one by one
+        BvhBuild B;
+        bvh_build(d->colliders, d->n_colliders, B);
+        int32_t *lin, *tri;
+        BvhNode* nodes;
+        if ((rc = upload(c, B.lin.data(), (int64_t)B.lin.size(), &lin))) return rc;
+        if ((rc = upload(c, B.tri.data(), (int64_t)B.tri.size(), &tri))) return rc;
+        if ((rc = upload(c, B.nodes.data(), (int64_t)B.nodes.size(), &nodes))) return rc;
+        S.nlin = (int)B.lin.size();
+        S.lin = (decltype(S.lin))lin;
+        S.bvh_tri = (decltype(S.bvh_tri))tri;
+        S.bvh = (decltype(S.bvh))nodes;
+        S.bvh_nodes = (int)B.nodes.size();
+    }
     int fan = 1;
     c->has_diffuse = 0;
     for (int i = 0; i < d->n_colliders; ++i)
@@ -1444,6 +1463,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     c->fanout = fan;
     c->mats = 0;
     for (int i = 0; i < d->n_materials; ++i) c->mats |= mat_bit(d->materials[i].type);
+    if (S.bvh_nodes > 0) c->mats |= MAT_BVH;
     c->chain_ok = true;
     c->hint_key[0] = -1;  // ray counts of another scene are no plan for this one
     c->has_scene = true;

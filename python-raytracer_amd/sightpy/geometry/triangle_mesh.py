@@ -1,9 +1,12 @@
 """OBJ triangle mesh (reference `geometry/triangle_mesh.py:12-43`).
 
-The reference constructor raises NameError (`colliders` undefined, :40).  This version builds one
-`Triangle_Collider` per face (vertex indices from 'f' records, 1-based, '/'-separated), which is
-what the reference intends.  Large meshes are intersected by the wave-cooperative kernel path
-(one ray per wave, triangles spread over lanes, `__shfl_xor` min reduction of packed (t, id)).
+The reference constructor raises NameError (`colliders` undefined, :40), and its header notes the
+missing bounding volume hierarchy (:7-9).  This version builds one `Triangle_Collider` per face
+(vertex indices from 'f' records, 1-based, '/'-separated), which is what the reference intends.
+On the device the Triangle colliders of a scene with 8 or more of them are intersected through a
+BVH built when the scene is uploaded (csrc/rt_bvh.h, traversal `bvh_nearest` / `bvh_shadow` in
+csrc/rt_device.h), with the same nearest / first-index / tie results as the linear loop over
+`scene.collider_list`.
 """
 from ..utils.vector3 import vec3
 from .primitive import Primitive

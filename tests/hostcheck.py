@@ -32,7 +32,31 @@ def lib():
         _lib.hc_mt_uniforms.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         _lib.hc_last_error.restype = ctypes.c_char_p
+        _lib.hc_set_bvh.argtypes = [ctypes.c_int]
+        _lib.hc_bvh_nodes.argtypes = [ctypes.POINTER(N.SceneDesc)]
     return _lib
+
+
+def set_bvh(on):
+    """1: large meshes through the BVH (the GPU's behaviour), 0: every collider in the linear loop."""
+    lib().hc_set_bvh(int(on))
+
+
+def bvh_nodes(scene):
+    L = lower_scene(scene)
+    return lib().hc_bvh_nodes(ctypes.byref(L.desc()))
+
+
+def nearest(scene, O, D):
+    """nearest_hit for rays (3, n): (t, collider id, orientation)."""
+    L = lower_scene(scene)
+    d = L.desc()
+    O = np.ascontiguousarray(O, dtype=np.float64)
+    D = np.ascontiguousarray(D, dtype=np.float64)
+    n = O.shape[1]
+    t, ids, orient = np.empty(n), np.empty(n, np.int32), np.empty(n)
+    lib().hc_nearest(ctypes.byref(d), N.ptr(O), N.ptr(D), n, N.ptr(t), N.ptr(ids), N.ptr(orient))
+    return t, ids, orient
 
 
 def render(scene, jitter, seed=0, rows=None):

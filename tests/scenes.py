@@ -9,7 +9,7 @@ tests/golden/gen_golden.py renders the reference's own scripts with the same ove
 import numpy as np
 
 from sightpy import (Scene, Sphere, Plane, Cuboid, Glossy, Refractive, ThinFilmInterference, Diffuse,
-                     Emissive, image, rgb, vec3)
+                     Emissive, TriangleMesh, image, rgb, vec3)
 
 
 def _depth(scene, depth):
@@ -156,4 +156,62 @@ def features(width=64, height=48, depth=4, sp=None):
     sc.add(sp.Sphere(material=metal, center=vec3(0.1, -0.25, 0.2), radius=0.25, max_ray_depth=depth))
     sc.add(sp.Sphere(material=lamp, center=vec3(1.5, 0.8, -2.0), radius=0.3, max_ray_depth=depth, shadow=False))
     sc.add_Background("miramar.jpeg", spherical=True)
+    return sc
+
+
+def write_icosphere_obj(path, subdiv=2, radius=0.5, duplicate_faces=0, slash_format=True):
+    """Write an icosphere as a Wavefront OBJ (v / f records, 1-based, 'i/t/n' face syntax when
+    `slash_format`).  `duplicate_faces` repeats the first faces at the end (exact ties: two
+    colliders at the same distance, both shaded by the reference, ray.py:131-146)."""
+    t = (1.0 + 5 ** 0.5) / 2.0
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    V = [np.array(v, dtype=np.float64) / np.linalg.norm(v) for v in V]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+         (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10),
+         (8, 6, 7), (9, 8, 1)]
+    for _ in range(subdiv):
+        mids = {}
+
+        def mid(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in mids:
+                m = V[a] + V[b]
+                V.append(m / np.linalg.norm(m))
+                mids[k] = len(V) - 1
+            return mids[k]
+
+        F = [f for a, b, c in F for f in ((a, mid(a, b), mid(c, a)), (b, mid(b, c), mid(a, b)),
+                                          (c, mid(c, a), mid(b, c)), (mid(a, b), mid(b, c), mid(c, a)))]
+    F = F + F[:duplicate_faces]
+    with open(path, "w") as fh:
+        fh.write("# icosphere, %d faces\n" % len(F))
+        for v in V:
+            fh.write("v %.17g %.17g %.17g\n" % tuple(radius * v))
+        for a, b, c in F:
+            if slash_format:
+                fh.write("f %d/%d/%d %d//%d %d\n" % (a + 1, a + 1, a + 1, b + 1, b + 1, c + 1))
+            else:
+                fh.write("f %d %d %d\n" % (a + 1, b + 1, c + 1))
+    return len(F)
+
+
+def mesh_scene(obj_path, width=64, height=48, depth=3):
+    """A TriangleMesh in the ex1 setting: a glossy icosphere mesh next to a
+    sphere over the textured floor, sky box background, one shadowing light."""
+    red = Glossy(diff_color=rgb(0.6, 0.1, 0.1), n=vec3(1.5 + 0.2j, 1.5 + 0.2j, 1.5 + 0.2j), roughness=0.2,
+                 spec_coeff=0.4, diff_coeff=0.8)
+    gold = Glossy(diff_color=rgb(1.0, 0.572, 0.184), n=vec3(0.15 + 3.58j, 0.4 + 2.37j, 1.54 + 1.91j),
+                  roughness=0.0, spec_coeff=0.2, diff_coeff=0.8)
+    floor = Glossy(diff_color=image("checkered_floor.png", repeat=20.0), n=vec3(1.2 + 0.3j, 1.2 + 0.3j, 1.1 + 0.3j),
+                   roughness=0.2, spec_coeff=0.3, diff_coeff=0.9)
+    sc = Scene(ambient_color=rgb(0.05, 0.05, 0.05))
+    sc.add_Camera(look_from=vec3(0.3, 0.6, 1.8), look_at=vec3(0.0, 0.0, -1.0), screen_width=width,
+                  screen_height=height)
+    sc.add_DirectionalLight(Ldir=vec3(0.52, 0.45, -0.5), color=rgb(0.5, 0.5, 0.5))
+    sc.add(Sphere(material=gold, center=vec3(-0.8, 0.0, -1.2), radius=0.45, max_ray_depth=depth))
+    sc.add(TriangleMesh(obj_path, center=vec3(0.35, 0.05, -1.0), material=red, max_ray_depth=depth))
+    sc.add(Plane(material=floor, center=vec3(0, -0.5, -2.0), width=40.0, height=40.0, u_axis=vec3(1.0, 0, 0),
+                 v_axis=vec3(0, 0, -1.0), max_ray_depth=depth))
+    sc.add_Background("stormydays.png")
     return sc

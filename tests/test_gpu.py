@@ -260,3 +260,40 @@ def test_gpu_async_frames_match_sync_frame():
     assert st.as_dict()["total_rays"] == ref.stats["total_rays"]
     np.testing.assert_allclose(rgb, ref.rgb, rtol=1e-12, atol=1e-15)
     assert np.array_equal(u8.reshape(120, 160, 3), ref.srgb8)
+
+
+@pytest.mark.parametrize("mode", ["wavefront", "frame"])
+def test_gpu_triangle_mesh_bvh_matches_oracle(tmp_path, mode):
+    """TriangleMesh through the device BVH (320 triangles + a tie-making duplicate set) against the
+    oracle's linear loop over the collider list: hit ids exact, per-depth counts, RGB."""
+    for dup in (0, 12):
+        path = str(tmp_path / ("ico%d.obj" % dup))
+        scenes.write_icosphere_obj(path, subdiv=2, duplicate_faces=dup)
+        sc = scenes.mesh_scene(path, 48, 36, 3)
+        np.random.seed(9)
+        jit = sc.camera.draw_jitter(2)
+        _set_option("frame_kernel", 1 if mode == "frame" else 0)
+        try:
+            out = _backend().render_scene(sc, 2, jitter=jit, seed=1, want_hits=True)
+        finally:
+            _set_option("frame_kernel", -1)
+        rgb, ids, counts = O.render_linear(sc, jit)
+        assert np.array_equal(out.hit_ids, ids)
+        assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+        np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
+
+
+def test_gpu_mesh_nearest_matches_oracle(tmp_path):
+    import test_mesh
+
+    path = str(tmp_path / "ico.obj")
+    scenes.write_icosphere_obj(path, subdiv=3)
+    sc = scenes.mesh_scene(path)
+    Oa, Da = test_mesh._probe_rays(sc, np.random.default_rng(3), n=20000)
+    from sightpy import vec3
+
+    t, ids, orient = _backend().nearest_hits(sc, vec3(*Oa), vec3(*Da))
+    near, ref = O.hit_ids(sc, Oa, Da)
+    assert np.array_equal(ids, ref)
+    hit = ref >= 0
+    assert np.array_equal(t[hit], near[hit])
