@@ -38,6 +38,8 @@ CONFIGS = {
     "example4_4k_d6": ("example4", 3840, 2160, 6, 10, "example4.py (thin film) 3840x2160 depth 6, 10 spp"),
     "cornell_800_s512": ("cornell", 800, 800, None, 512, "example_cornellbox.py 800x800, 512 spp (MC)"),
     "example1_400x300_d3": ("example1", 400, 300, None, 6, "example1.py 400x300 depth 3, 6 spp"),
+    "mesh_1080p_d3": ("mesh_bench", 1920, 1080, 3, 2,
+                      "TriangleMesh (20480-triangle icosphere, BVH) + sphere + floor + sky 1920x1080 depth 3, 2 spp"),
 }
 
 

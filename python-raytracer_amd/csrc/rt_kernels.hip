@@ -1054,6 +1054,7 @@ struct srt_ctx {
     // ex1 1080p d5 13388 vs 10478, ex3 1080p d8 8950 vs 9585, ex4 4K d6 14081 vs 17494,
     // cornell 800x800 512 spp 3542 vs 4073.
     int use_frame = -1;
+    bool use_bvh = true;  // option "bvh": 0 intersects mesh triangles one by one (comparison runs)
     // chain mode of the wavefront path (single-child scenes): from the first depth >= 2 whose ray
     // count in the previous frame of the same shape was below chain_rays
     int64_t chain_rays = 1000000;
@@ -1361,6 +1362,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
     if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
     if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
+    if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
@@ -1434,7 +1436,11 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     {
         // triangle meshes: BVH over the Triangle colliders, the rest intersected one by one
         BvhBuild B;
-        bvh_build(d->colliders, d->n_colliders, B);
+        if (c->use_bvh) {
+            bvh_build(d->colliders, d->n_colliders, B);
+        } else {
+            for (int i = 0; i < d->n_colliders; ++i) B.lin.push_back(i);
+        }
         int32_t *lin, *tri;
         BvhNode* nodes;
         if ((rc = upload(c, B.lin.data(), (int64_t)B.lin.size(), &lin))) return rc;

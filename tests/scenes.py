@@ -215,3 +215,14 @@ def mesh_scene(obj_path, width=64, height=48, depth=3):
                  v_axis=vec3(0, 0, -1.0), max_ray_depth=depth))
     sc.add_Background("stormydays.png")
     return sc
+
+
+def mesh_bench(width=1920, height=1080, depth=3, subdiv=5):
+    """Bench workload for the BVH: mesh_scene with an icosphere of 20 * 4**subdiv triangles."""
+    import os
+    import tempfile
+
+    path = os.path.join(tempfile.gettempdir(), "sightpy_icosphere_%d.obj" % subdiv)
+    if not os.path.exists(path):
+        write_icosphere_obj(path, subdiv=subdiv)
+    return mesh_scene(path, width, height, depth)
