@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 2
+#define SRT_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------------------------ */
 #define SRT_OK 0
@@ -165,6 +165,9 @@ typedef struct srt_scene_desc {
     double ambient[3];         /* scene.ambient_color */
     int32_t max_ray_depth;     /* max over colliders (depth cap = this + 1, +2 with Diffuse) */
     int32_t has_diffuse;
+    uint64_t texel_key;        /* caller's identity of the texel pool (0 = none): when it and
+                                  texel_bytes equal the resident pool's, the pool stays in HBM and is
+                                  not copied again (frame sequences re-upload only the small tables) */
 } srt_scene_desc;
 
 /* ---- camera / render ------------------------------------------------------------------ */

@@ -1055,6 +1055,10 @@ struct srt_ctx {
     // cornell 800x800 512 spp 3542 vs 4073.
     int use_frame = -1;
     bool use_bvh = true;  // option "bvh": 0 intersects mesh triangles one by one (comparison runs)
+    // texel pool (outside scene_bufs: survives re-uploads with the same texel_key)
+    uint8_t* texels = nullptr;
+    uint64_t texel_key = 0;
+    int64_t texel_bytes = 0;
     // chain mode of the wavefront path (single-child scenes): from the first depth >= 2 whose ray
     // count in the previous frame of the same shape was below chain_rays
     int64_t chain_rays = 1000000;
@@ -1348,7 +1352,7 @@ int srt_destroy(srt_ctx* c) {
     free_list(c->queue_bufs);
     free_list(c->ring_bufs);
     void* bufs[] = {c->fb, c->rgb, c->u8, c->xs, c->ys, c->rows, c->jit, c->hit, c->counts, c->flags, c->shadow,
-                    c->mt, c->mt_out};
+                    c->mt, c->mt_out, c->texels};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1419,7 +1423,23 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     if ((rc = upload(c, d->colliders, d->n_colliders, &col))) return rc;
     if ((rc = upload(c, d->materials, d->n_materials, &mat))) return rc;
     if ((rc = upload(c, d->textures, d->n_textures, &tex))) return rc;
-    if ((rc = upload(c, d->texels, d->texel_bytes, &texels))) return rc;
+    // texel pool: kept in HBM across uploads while the caller's key and size are unchanged
+    if (d->texel_key != 0 && d->texel_key == c->texel_key && d->texel_bytes == c->texel_bytes && c->texels) {
+        texels = c->texels;
+    } else {
+        if (c->texels) (void)hipFree(c->texels);
+        c->texels = nullptr;
+        c->texel_key = 0;
+        c->texel_bytes = 0;
+        texels = nullptr;
+        if (d->texel_bytes > 0 && d->texels) {
+            HIP_TRY(dalloc(&texels, d->texel_bytes));
+            HIP_TRY(hipMemcpy(texels, d->texels, (size_t)d->texel_bytes, hipMemcpyDefault));
+            c->texels = texels;
+            c->texel_key = d->texel_key;
+            c->texel_bytes = d->texel_bytes;
+        }
+    }
     if ((rc = upload(c, d->lights, d->n_lights, &lights))) return rc;
     if ((rc = upload(c, d->media, (int64_t)d->n_media * 6, &media))) return rc;
     if ((rc = upload(c, d->glossy_f0, (int64_t)d->n_materials * d->n_media * 3, &f0))) return rc;

@@ -56,6 +56,7 @@ class Lowered:
         self.has_diffuse = 0
         self.media_keys = []
         self.scene_n = None
+        self.texel_key = 0
 
     def desc(self):
         d = N.SceneDesc()
@@ -78,6 +79,7 @@ class Lowered:
         d.ambient[:] = list(self.ambient)
         d.max_ray_depth = int(self.max_ray_depth)
         d.has_diffuse = int(self.has_diffuse)
+        d.texel_key = int(self.texel_key)
         return d
 
     def signature(self):
@@ -85,7 +87,7 @@ class Lowered:
                  self.lights.tobytes(), self.media.tobytes(), self.glossy_f0.tobytes(),
                  self.light_local.tobytes(), self.importance.tobytes(), repr(self.ambient).encode(),
                  str(self.max_ray_depth).encode()]
-        return hash((tuple(parts), self.texels.size, int(self.texels[:: max(1, self.texels.size // 4096)].sum())))
+        return hash((tuple(parts), self.texels.size, self.texel_key))
 
 
 class _TexturePool:
@@ -102,7 +104,12 @@ class _TexturePool:
         if u8.ndim == 2:
             u8 = u8[:, :, None]
         if u8.shape[2] < 3:  # grey images: replicate to RGB (device reads 3 channels per texel)
-            u8 = np.ascontiguousarray(np.repeat(u8[:, :, :1], 3, axis=2))
+            src = u8
+            hit = _GREY_CACHE.get(id(src))
+            if hit is None or hit[0] is not src:
+                hit = (src, np.ascontiguousarray(np.repeat(src[:, :, :1], 3, axis=2)))
+                _GREY_CACHE[id(src)] = hit  # (keeps src alive, so its id stays unique)
+            u8 = hit[1]
         key = id(u8) if u8.base is None else (id(u8.base), u8.__array_interface__["data"][0])
         if key not in self.offsets:
             self.offsets[key] = self.size
@@ -119,10 +126,30 @@ class _TexturePool:
         self.records.append(rec)
         return len(self.records) - 1
 
+    def key(self):
+        """Identity of the pool's images (the same image objects, in the same order)."""
+        if not self.images:
+            return 0
+        ident = tuple((id(im), im.__array_interface__["data"][0], im.shape) for im in self.images)
+        return hash(ident) & (2**64 - 1) or 1
+
     def finish(self):
+        """Records and the concatenated texel pool.  The pool of the last key is cached: a frame
+        sequence (create_animation) re-lowers its scene every frame with the same images, and the
+        device keeps the resident copy for an unchanged texel_key (srt_upload_scene)."""
         tex = np.array(self.records, dtype=N.TEXTURE_DTYPE) if self.records else np.zeros(0, N.TEXTURE_DTYPE)
+        key = self.key()
+        cached = _POOL_CACHE.get("pool")
+        if cached is not None and cached[0] == key and key != 0:
+            return tex, cached[1], key
         texels = np.concatenate([im.reshape(-1) for im in self.images]) if self.images else np.zeros(0, np.uint8)
-        return tex, texels
+        # the cache holds the images too, so their ids cannot be reused by other arrays meanwhile
+        _POOL_CACHE["pool"] = (key, texels, list(self.images))
+        return tex, texels, key
+
+
+_POOL_CACHE = {}
+_GREY_CACHE = {}
 
 
 def _medium_f0(n_ray, n_mat):
@@ -376,6 +403,6 @@ def lower_scene(scene, extra_media=()):
         med[k, 3:6] = [v.imag for v in cv]
     L.media = med
     L.media_keys = keys
-    L.textures, L.texels = pool.finish()
+    L.textures, L.texels, L.texel_key = pool.finish()
     L.ambient = tuple(_f3(scene.ambient_color))
     return L

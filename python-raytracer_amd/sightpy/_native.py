@@ -101,6 +101,7 @@ class SceneDesc(ctypes.Structure):
         ("ambient", _d3),
         ("max_ray_depth", ctypes.c_int32),
         ("has_diffuse", ctypes.c_int32),
+        ("texel_key", ctypes.c_uint64),
     ]
 
 
@@ -189,7 +190,7 @@ class TraceArgs(ctypes.Structure):
 
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
 RENDER_ASYNC = 1  # SRT_RENDER_ASYNC
-ABI_VERSION = 2  # SRT_ABI_VERSION of include/sightpy_rt.h
+ABI_VERSION = 3  # SRT_ABI_VERSION of include/sightpy_rt.h
 
 SIGNATURES = {
     "srt_abi_version": (ctypes.c_int, []),

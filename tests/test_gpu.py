@@ -297,3 +297,28 @@ def test_gpu_mesh_nearest_matches_oracle(tmp_path):
     assert np.array_equal(ids, ref)
     hit = ref >= 0
     assert np.array_equal(t[hit], near[hit])
+
+
+def test_gpu_create_animation_frames(tmp_path, monkeypatch):
+    """create_animation (persistent device scene, background frame writer) writes the same frames
+    as rendering them one by one."""
+    from PIL import Image
+    from sightpy import create_animation, vec3
+
+    monkeypatch.chdir(tmp_path)
+
+    def update(scene, t):
+        scene.collider_list[0].center = vec3(-0.75 + t, 0.1, -3.0)
+
+    sc = scenes.example1(48, 36, 3)
+    np.random.seed(4)
+    create_animation(sc, 1, 3, 0.0, 1.0, update, "anim")
+    sc2 = scenes.example1(48, 36, 3)
+    np.random.seed(4)
+    t = 0.0
+    for i in range(3):
+        update(sc2, t)
+        ref = np.array(sc2.render(1))
+        got = np.array(Image.open(tmp_path / "frames" / ("anim_%d.png" % i)))
+        assert np.array_equal(got, ref), i
+        t += 1.0 / 3

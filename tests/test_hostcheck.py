@@ -44,3 +44,21 @@ def test_device_math_cornell_statistics():
     assert np.array_equal(hits[0], g["hit_id"][0])
     ref_mean, got_mean = g["rgb"].mean(), rgb.mean()
     assert abs(got_mean - ref_mean) / ref_mean < 0.15, (got_mean, ref_mean)
+
+
+def test_texel_pool_persists_across_lowerings():
+    """Frame sequences re-lower the scene every frame: same images -> same texel_key and the cached
+    pool (the device then keeps its copy); another image -> another key."""
+    from sightpy._lower import lower_scene
+    from sightpy import image
+
+    sc = scenes.example1(16, 12)
+    a, b = lower_scene(sc), lower_scene(sc)
+    assert a.texel_key == b.texel_key != 0
+    assert a.texels is b.texels
+    assert a.signature() == b.signature()
+    sc.collider_list[0].assigned_primitive.center.x = sc.collider_list[0].assigned_primitive.center.x + 0.0
+    floor = sc.collider_list[2].assigned_primitive.material
+    floor.diff_texture = image("wood.jpg", repeat=80.0)
+    c = lower_scene(sc)
+    assert c.texel_key != a.texel_key and c.texels.size != a.texels.size
