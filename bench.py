@@ -203,9 +203,19 @@ def main():
         # each rank's uint8 tile, padded to the largest shard: the send buffer of the all-gather
         tiles = [torch.zeros((max_shard_rows(H, world), W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
         gather = RowGather(H, world, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
+    streams = {}
+
+    def frame_stream():
+        """torch handle of the stream the library queued its last frame on (pipelined frames
+        alternate between two streams)."""
+        import torch
+
         sp = ctypes.c_void_p()
         N.check(lib, lib.srt_stream(ctx, ctypes.byref(sp)))
-        lib_stream = torch.cuda.ExternalStream(sp.value, device=torch.device("cuda", dev))
+        if sp.value not in streams:
+            streams[sp.value] = torch.cuda.ExternalStream(sp.value, device=torch.device("cuda", dev))
+        return streams[sp.value]
+
     frame = {"k": 0}
 
     def step(st, async_ok=True):
@@ -215,17 +225,19 @@ def main():
                                                   jit_dev, N.ptr(mt_key_out), ctypes.byref(mt_pos_out)))
         i = frame["k"] % 2
         frame["k"] += 1
+        a.flags = N.RENDER_ASYNC if (pipelined and async_ok) else 0
         if tiles is not None:
             if done[i] is not None:
-                lib_stream.wait_event(done[i])  # the gather that read this tile two frames ago
+                # the gather that read this tile two frames ago must be done before this frame's
+                # resolve overwrites it (a host wait: two frames later it has long finished)
+                done[i].synchronize()
             a.out_srgb8 = ctypes.c_void_p(tiles[i].data_ptr())
-        a.flags = N.RENDER_ASYNC if (pipelined and async_ok) else 0
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
         if tiles is not None:
             import torch
 
             cur = torch.cuda.current_stream()
-            cur.wait_stream(lib_stream)  # this frame's tile is complete
+            cur.wait_stream(frame_stream())  # this frame's tile is complete
             if backend == "nccl":
                 frame["image"] = gather(tiles[i])
             else:

@@ -1003,9 +1003,48 @@ struct FramePlan {
     int64_t cnt_words = 0, pass_words = 0;
 };
 
+// Buffers and stream of one frame in flight.  Synchronous calls use slot 0; pipelined
+// (SRT_RENDER_ASYNC) frames alternate between the two slots, each with its own stream, so one
+// frame's low-occupancy tail (deep depths, resolve) overlaps the next frame's primary kernel.
+struct FrameSlot {
+    hipStream_t stream = nullptr;
+    // ray queues: 2 x NSHARD segments of `seg` rays
+    Queue q[2]{};
+    int64_t seg = 0;
+    std::vector<void*> queue_bufs;
+    // frame kernel rings (k_frame): nslot rings of ring_cap rays, one lock word per ring
+    Queue ring{};
+    int64_t ring_cap = 0;
+    int nslot = 0;
+    uint32_t* ring_lock = nullptr;
+    std::vector<void*> ring_bufs;
+    // frame buffers
+    double* fb = nullptr;
+    int64_t fb_cap = 0;
+    double* rgb = nullptr;
+    int64_t rgb_cap = 0;
+    uint8_t* u8 = nullptr;
+    int64_t u8_cap = 0;
+    double* jit = nullptr;
+    int64_t jit_cap = 0;
+    int32_t* hit = nullptr;
+    int64_t hit_cap = 0;
+    uint32_t* counts = nullptr;  // [SRT_MAX_DEPTHS][NSHARD]
+    uint32_t* flags = nullptr;   // [2]
+    unsigned long long* shadow = nullptr;  // [NSHARD]
+    std::vector<hipEvent_t> ev;
+    uint32_t* host = nullptr;  // pinned: per-pass counters/flags, shadow count
+    int64_t host_words = 0;
+    // counts/flags/shadow are zeroed by the kernels that consume them (k_pass_end, k_resolve); a
+    // frame that did not complete leaves them dirty and the next one clears them first
+    bool dirty = true;
+    // asynchronous frames queued on this slot since the last synchronisation point
+    int pending = 0;
+    FramePlan plan;
+};
+
 struct srt_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
     int max_blocks = 2048;
     int64_t queue_budget = (int64_t)96 << 30;  // bytes for both ray queues
     // scene
@@ -1016,63 +1055,37 @@ struct srt_ctx {
     int fanout = 1;
     uint32_t mats = 0;  // material types present (selects the kernel variant)
     std::vector<void*> scene_bufs;
-    // ray queues: 2 x NSHARD segments of `seg` rays
-    Queue q[2]{};
-    int64_t seg = 0;
-    std::vector<void*> queue_bufs;
-    // frame
-    double* fb = nullptr;
-    int64_t fb_cap = 0;
-    double* rgb = nullptr;
-    int64_t rgb_cap = 0;
-    uint8_t* u8 = nullptr;
-    int64_t u8_cap = 0;
+    // texel pool (outside scene_bufs: survives re-uploads with the same texel_key)
+    uint8_t* texels = nullptr;
+    uint64_t texel_key = 0;
+    int64_t texel_bytes = 0;
+    // camera tables (shared by the slots; uploaded only when they change)
     double* xs = nullptr;
     double* ys = nullptr;
     int32_t* rows = nullptr;
     int64_t cam_cap[3] = {0, 0, 0};
     std::vector<uint8_t> cam_host[3];  // host copies of what xs / ys / rows hold
-    double* jit = nullptr;
-    int64_t jit_cap = 0;
-    int32_t* hit = nullptr;
-    int64_t hit_cap = 0;
-    uint32_t* counts = nullptr;  // [SRT_MAX_DEPTHS][NSHARD]
-    uint32_t* flags = nullptr;   // [2]
-    unsigned long long* shadow = nullptr;
-    std::vector<hipEvent_t> ev;
     uint32_t* mt = nullptr;    // MT19937 jump tables (31 x 624) + two round keys + the final key
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
-    uint32_t* host = nullptr;  // pinned: per-pass counters/flags, shadow count
-    int64_t host_words = 0;
-    // counts/flags/shadow are zeroed by the kernels that consume them (k_pass_end, k_resolve); a
-    // frame that did not complete leaves them dirty and the next one clears them first
-    bool dirty = true;
-    // frame kernel rings (k_frame): nslot rings of ring_cap rays, one lock word per ring
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
     // per-depth wavefront kernels otherwise.  Measured (one MI355X, Mrays/s, wavefront vs frame):
     // ex1 1080p d5 13388 vs 10478, ex3 1080p d8 8950 vs 9585, ex4 4K d6 14081 vs 17494,
     // cornell 800x800 512 spp 3542 vs 4073.
     int use_frame = -1;
     bool use_bvh = true;  // option "bvh": 0 intersects mesh triangles one by one (comparison runs)
-    // texel pool (outside scene_bufs: survives re-uploads with the same texel_key)
-    uint8_t* texels = nullptr;
-    uint64_t texel_key = 0;
-    int64_t texel_bytes = 0;
-    // chain mode of the wavefront path (single-child scenes): from the first depth >= 2 whose ray
+    // chain mode of the wavefront path (single-child scenes): from the first depth >= 1 whose ray
     // count in the previous frame of the same shape was below chain_rays
     int64_t chain_rays = 1000000;
     bool chain_ok = true;  // cleared when a tie produced a second child in chain mode
     int64_t hint_key[3] = {-1, -1, -1};
     int64_t hint[SRT_MAX_DEPTHS] = {};
-    Queue ring{};
-    int64_t ring_cap = 0;
-    int nslot = 0;
-    uint32_t* ring_lock = nullptr;
-    std::vector<void*> ring_bufs;
-    // asynchronous frames (SRT_RENDER_ASYNC) in flight since the last synchronisation point
-    int async_pending = 0;
-    FramePlan async_plan;
+    // frame slots; `f` is the one the current call works on
+    FrameSlot slots[2];
+    FrameSlot* f = &slots[0];
+    int next_slot = 0;      // slot of the next asynchronous frame
+    int last_slot = 0;      // slot of the last asynchronous frame (its stats are reported)
+    int async_pending = 0;  // asynchronous frames in flight (both slots)
     srt_stats async_stats{};
 };
 
@@ -1088,24 +1101,24 @@ void free_list(std::vector<void*>& v) {
 int ensure_queues(srt_ctx* c, int64_t rays) {
     int64_t seg = (rays + NSHARD - 1) / NSHARD;
     seg = seg + seg / 8 + 1024;
-    if (seg <= c->seg) return SRT_OK;
-    free_list(c->queue_bufs);
-    c->seg = 0;
+    if (seg <= c->f->seg) return SRT_OK;
+    free_list(c->f->queue_bufs);
+    c->f->seg = 0;
     const int64_t n = seg * NSHARD;
     for (int k = 0; k < 2; ++k) {
-        Queue& q = c->q[k];
+        Queue& q = c->f->q[k];
         double** dptr[9] = {&q.ox, &q.oy, &q.oz, &q.dx, &q.dy, &q.dz, &q.wr, &q.wg, &q.wb};
         for (double** p : dptr) {
             if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray queue allocation failed");
-            c->queue_bufs.push_back(*p);
+            c->f->queue_bufs.push_back(*p);
         }
         uint32_t** uptr[3] = {&q.pix, &q.meta, &q.path};
         for (uint32_t** p : uptr) {
             if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray queue allocation failed");
-            c->queue_bufs.push_back(*p);
+            c->f->queue_bufs.push_back(*p);
         }
     }
-    c->seg = seg;
+    c->f->seg = seg;
     return SRT_OK;
 }
 
@@ -1117,27 +1130,27 @@ int ensure_ring(srt_ctx* c, int64_t cap) {
     cap = k;
     int dev_cus = c->max_blocks / 8;
     const int nslot = std::max(1024, 2 * 32 * dev_cus);
-    if (cap <= c->ring_cap && nslot <= c->nslot) return SRT_OK;
-    free_list(c->ring_bufs);
-    c->ring_cap = 0;
-    c->nslot = 0;
+    if (cap <= c->f->ring_cap && nslot <= c->f->nslot) return SRT_OK;
+    free_list(c->f->ring_bufs);
+    c->f->ring_cap = 0;
+    c->f->nslot = 0;
     const int64_t n = cap * nslot;
-    Queue& q = c->ring;
+    Queue& q = c->f->ring;
     double** dptr[9] = {&q.ox, &q.oy, &q.oz, &q.dx, &q.dy, &q.dz, &q.wr, &q.wg, &q.wb};
     for (double** p : dptr) {
         if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray ring allocation failed");
-        c->ring_bufs.push_back(*p);
+        c->f->ring_bufs.push_back(*p);
     }
     uint32_t** uptr[3] = {&q.pix, &q.meta, &q.path};
     for (uint32_t** p : uptr) {
         if (dalloc(p, n) != hipSuccess) return fail(SRT_ERR_MEMORY, "ray ring allocation failed");
-        c->ring_bufs.push_back(*p);
+        c->f->ring_bufs.push_back(*p);
     }
-    if (dalloc(&c->ring_lock, nslot) != hipSuccess) return fail(SRT_ERR_MEMORY, "ring lock allocation failed");
-    c->ring_bufs.push_back(c->ring_lock);
-    HIP_TRY(hipMemset(c->ring_lock, 0, (size_t)nslot * 4));
-    c->ring_cap = cap;
-    c->nslot = nslot;
+    if (dalloc(&c->f->ring_lock, nslot) != hipSuccess) return fail(SRT_ERR_MEMORY, "ring lock allocation failed");
+    c->f->ring_bufs.push_back(c->f->ring_lock);
+    HIP_TRY(hipMemset(c->f->ring_lock, 0, (size_t)nslot * 4));
+    c->f->ring_cap = cap;
+    c->f->nslot = nslot;
     return SRT_OK;
 }
 
@@ -1182,9 +1195,9 @@ int check_flags(uint32_t f0) {
 TraceParams base_params(srt_ctx* c, uint64_t seed) {
     TraceParams P{};
     P.S = c->S;
-    P.flags = c->flags;
-    P.shadow = c->shadow;
-    P.seg = c->seg;
+    P.flags = c->f->flags;
+    P.shadow = c->f->shadow;
+    P.seg = c->f->seg;
     P.seed = seed;
     return P;
 }
@@ -1200,15 +1213,31 @@ int trace_grid(const srt_ctx* c) { return std::max(NSHARD, (c->max_blocks / NSHA
 
 // copy `bytes` from host `src` to device `dst` unless `shadow` (the host copy of what dst holds)
 // already equals it.  The shadow is invalidated whenever the buffer is reallocated (ensure_buf).
+int finish_async(srt_ctx* c, srt_stats* st);
+
+// the camera tables are shared by the frame slots: wait for the frames in flight before changing
+// them (keeps the current slot)
+int quiesce_for_shared_write(srt_ctx* c) {
+    if (c->async_pending == 0) return SRT_OK;
+    FrameSlot* keep = c->f;
+    int rc = finish_async(c, nullptr);
+    c->f = keep;
+    return rc;
+}
+
 int upload_if_changed(srt_ctx* c, void* dst, std::vector<uint8_t>& shadow, const void* src, size_t bytes) {
     if (is_device_ptr(src)) {
+        int rc = quiesce_for_shared_write(c);
+        if (rc) return rc;
         shadow.clear();
-        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->f->stream));
         return SRT_OK;
     }
     if (shadow.size() == bytes && !memcmp(shadow.data(), src, bytes)) return SRT_OK;
+    int rc = quiesce_for_shared_write(c);
+    if (rc) return rc;
     shadow.assign((const uint8_t*)src, (const uint8_t*)src + bytes);
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->f->stream));
     return SRT_OK;
 }
 
@@ -1229,7 +1258,7 @@ constexpr int SRT_RETRY_OVERFLOW = 1;
 int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
     bool overflow = false;
     for (int p = 0; p < F.npass; ++p) {
-        const uint32_t* hp = c->host + p * F.pass_words;
+        const uint32_t* hp = c->f->host + p * F.pass_words;
         int rc;
         if ((rc = check_flags(hp[F.cnt_words]))) return rc;
         overflow |= hp[F.cnt_words + 1] != 0;
@@ -1239,8 +1268,8 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
     double ms_trace = 0.0, ms_primary = 0.0;
     for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.rays_per_depth[d] = 0;
     for (int p = 0; p < F.npass; ++p) {
-        const uint32_t* hp = c->host + p * F.pass_words;
-        if (depth_total(hp + (int64_t)(F.dcap + 1) * NSHARD, F.frame ? INT64_MAX : c->seg) != 0)
+        const uint32_t* hp = c->f->host + p * F.pass_words;
+        if (depth_total(hp + (int64_t)(F.dcap + 1) * NSHARD, F.frame ? INT64_MAX : c->f->seg) != 0)
             return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
         if (F.frame) {
             // k_frame counts every ray it traces (per shard), depth 0 included
@@ -1248,16 +1277,16 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
                 for (int k = 0; k < NSHARD; ++k) S.rays_per_depth[d] += hp[(int64_t)d * NSHARD + k];
         } else {
             S.rays_per_depth[0] += (int64_t)std::min(F.batch, F.spp - p * F.batch) * F.npix;
-            for (int d = 1; d <= F.dcap; ++d) S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, c->seg);
+            for (int d = 1; d <= F.dcap; ++d) S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, c->f->seg);
         }
-        const hipEvent_t* ev = c->ev.data() + (int64_t)p * F.nev;
+        const hipEvent_t* ev = c->f->ev.data() + (int64_t)p * F.nev;
         float ms;
         HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
         ms_primary += ms;
         HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[F.chain_from > 0 ? F.chain_from + 1 : F.dcap + 1]));
         ms_trace += ms;
     }
-    const uint32_t* hshadow = c->host + F.npass * F.pass_words;
+    const uint32_t* hshadow = c->f->host + F.npass * F.pass_words;
     S.passes = F.npass;
     S.ms_trace_kernels = ms_trace;
     S.ms_primary_kernel = ms_primary;
@@ -1277,33 +1306,77 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
 // zero the pinned flag words of every pass (only while no frame is in flight)
 void clear_host_flags(srt_ctx* c, const FramePlan& F) {
     for (int p = 0; p < F.npass; ++p) {
-        c->host[p * F.pass_words + F.cnt_words] = 0u;
-        c->host[p * F.pass_words + F.cnt_words + 1] = 0u;
+        c->f->host[p * F.pass_words + F.cnt_words] = 0u;
+        c->f->host[p * F.pass_words + F.cnt_words + 1] = 0u;
     }
+}
+
+// Stream and counters of a slot, created on first use.
+int ensure_slot(FrameSlot& f) {
+    if (f.stream) return SRT_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
+    HIP_TRY(dalloc(&f.counts, SRT_MAX_DEPTHS * NSHARD));
+    HIP_TRY(dalloc(&f.flags, 2));
+    HIP_TRY(dalloc(&f.shadow, NSHARD));
+    f.dirty = true;
+    return SRT_OK;
+}
+
+void free_slot(FrameSlot& f) {
+    if (!f.stream) return;
+    (void)hipStreamSynchronize(f.stream);
+    free_list(f.queue_bufs);
+    free_list(f.ring_bufs);
+    void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
+    if (f.host) (void)hipHostFree(f.host);
+    (void)hipStreamDestroy(f.stream);
+    f = FrameSlot{};
 }
 
 // Wait for the asynchronous frames in flight and check them (flags accumulated over all of them,
 // stats of the last).  An overflow grows the queues and is reported as an error: those frames are
-// wrong and must be rendered again.
+// wrong and must be rendered again.  Leaves slot 0 current.
 int finish_async(srt_ctx* c, srt_stats* st) {
     if (c->async_pending == 0) {
+        c->f = &c->slots[0];
         if (st) *st = c->async_stats;
         return SRT_OK;
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (FrameSlot& f : c->slots)
+        if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
     c->async_pending = 0;
-    srt_stats S{};
-    int rc = collect_frame(c, c->async_plan, S);
-    clear_host_flags(c, c->async_plan);
-    if (rc == SRT_RETRY_OVERFLOW) {
-        if ((rc = c->async_plan.frame ? ensure_ring(c, 2 * c->ring_cap) : ensure_queues(c, 2 * c->seg * NSHARD)))
-            return rc;
+    int first_err = SRT_OK;
+    bool overflow = false;
+    srt_stats last{};
+    for (int k = 0; k < 2; ++k) {
+        FrameSlot& f = c->slots[(c->last_slot + 1 + k) % 2];  // the last frame's slot last
+        if (!f.pending) continue;
+        c->f = &f;
+        srt_stats S{};
+        int rc = collect_frame(c, f.plan, S);
+        clear_host_flags(c, f.plan);
+        f.pending = 0;
+        if (rc == SRT_RETRY_OVERFLOW) {
+            overflow = true;
+            if ((rc = f.plan.frame ? ensure_ring(c, 2 * f.ring_cap) : ensure_queues(c, 2 * f.seg * NSHARD))) {
+                first_err = first_err ? first_err : rc;
+            }
+        } else if (rc) {
+            first_err = first_err ? first_err : rc;
+        } else {
+            last = S;
+        }
+    }
+    c->f = &c->slots[0];
+    if (first_err) return first_err;
+    if (overflow)
         return fail(SRT_ERR_MEMORY, "a ray queue overflowed during an asynchronous frame (queues grown; render "
                                     "that frame again)");
-    }
-    if (rc) return rc;
-    c->async_stats = S;
-    if (st) *st = S;
+    c->async_stats = last;
+    if (st) *st = last;
     return SRT_OK;
 }
 
@@ -1336,10 +1409,11 @@ int srt_create(int device, srt_ctx** out) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
     c->max_blocks = prop.multiProcessorCount * 8;
-    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIP_TRY(dalloc(&c->counts, SRT_MAX_DEPTHS * NSHARD));
-    HIP_TRY(dalloc(&c->flags, 2));
-    HIP_TRY(dalloc(&c->shadow, NSHARD));
+    int rc = ensure_slot(c->slots[0]);
+    if (rc) {
+        delete c;
+        return rc;
+    }
     *out = c;
     return SRT_OK;
 }
@@ -1347,17 +1421,11 @@ int srt_create(int device, srt_ctx** out) {
 int srt_destroy(srt_ctx* c) {
     if (!c) return SRT_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    for (FrameSlot& f : c->slots) free_slot(f);
     free_list(c->scene_bufs);
-    free_list(c->queue_bufs);
-    free_list(c->ring_bufs);
-    void* bufs[] = {c->fb, c->rgb, c->u8, c->xs, c->ys, c->rows, c->jit, c->hit, c->counts, c->flags, c->shadow,
-                    c->mt, c->mt_out, c->texels};
+    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
-    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-    if (c->host) (void)hipHostFree(c->host);
-    (void)hipStreamDestroy(c->stream);
     delete c;
     return SRT_OK;
 }
@@ -1409,7 +1477,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     HIP_TRY(hipSetDevice(c->device));
     int rc0 = finish_async(c, nullptr);  // frames in flight read the scene tables freed below
     if (rc0) return rc0;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
     free_list(c->scene_bufs);
     c->has_scene = false;
     SceneView S{};
@@ -1548,16 +1616,30 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         for (int d = 1; d <= F.dcap; ++d)
             if (c->hint[d] < c->chain_rays) { F.chain_from = d; break; }
     }
-    // frames in flight use the buffers below: a synchronous frame, or one that would reallocate
-    // anything, first waits for them (and reports their errors)
-    if (c->async_pending > 0) {
+    // the slot of this frame: slot 0 for a synchronous frame (after the frames in flight),
+    // alternating slots for asynchronous ones
+    if (!async) {
+        if ((rc = finish_async(c, nullptr))) return rc;
+    } else {
+        FrameSlot& f = c->slots[c->next_slot];
+        if ((rc = ensure_slot(f))) return rc;
+        c->f = &f;
+    }
+    // frames in flight use the buffers below: a frame that would reallocate anything first waits
+    // for them (and reports their errors)
+    if (async && c->async_pending > 0) {
+        const FramePlan& pp = c->f->pending ? c->f->plan : c->slots[c->last_slot].plan;
         const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && a->n_rows <= c->cam_cap[2] &&
-                          3 * npix <= c->fb_cap && 3 * npix <= c->rgb_cap && 3 * npix <= c->u8_cap &&
-                          (int64_t)batch * npix * c->fanout <= c->seg * NSHARD && F.npass == c->async_plan.npass &&
-                          F.dcap == c->async_plan.dcap && F.frame == c->async_plan.frame &&
-                          F.chain_from == c->async_plan.chain_from;
-        if (!async || !same)
+                          3 * npix <= c->f->fb_cap && 3 * npix <= c->f->rgb_cap && 3 * npix <= c->f->u8_cap &&
+                          (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
+                          (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
+                          F.frame == pp.frame && F.chain_from == pp.chain_from &&
+                          (int)c->f->ev.size() >= F.npass * F.nev && c->f->host_words >= F.npass * F.pass_words + 2;
+        if (!same) {
+            FrameSlot* keep = c->f;
             if ((rc = finish_async(c, nullptr))) return rc;
+            c->f = keep;
+        }
     }
     {
         const void* old[3] = {c->xs, c->ys, c->rows};
@@ -1573,52 +1655,71 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     if ((rc = upload_if_changed(c, c->ys, c->cam_host[1], cam->ys, (size_t)cam->height * 8))) return rc;
     if ((rc = upload_if_changed(c, c->rows, c->cam_host[2], a->rows ? a->rows : rows_h.data(), (size_t)a->n_rows * 4)))
         return rc;
-    if ((rc = ensure_buf(&c->fb, c->fb_cap, 3 * npix))) return rc;
-    if ((rc = ensure_buf(&c->rgb, c->rgb_cap, 3 * npix))) return rc;
-    if ((rc = ensure_buf(&c->u8, c->u8_cap, 3 * npix))) return rc;
-    if (a->jitter && !jit_dev && (rc = ensure_buf(&c->jit, c->jit_cap, (int64_t)batch * 4 * npix))) return rc;
-    if (a->out_hit_id && !hit_dev && (rc = ensure_buf(&c->hit, c->hit_cap, (int64_t)batch * npix))) return rc;
-    if (F.frame) {
-        if ((rc = ensure_ring(c, (int64_t)FRAME_BLOCK * (c->fanout + 2) * 2))) return rc;
-    } else if ((rc = ensure_queues(c, (int64_t)batch * npix * c->fanout))) {
-        return rc;
-    }
-    if ((int)c->ev.size() < F.npass * F.nev) {
-        for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-        c->ev.assign(F.npass * F.nev, nullptr);
-        for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
-    }
-    // per-pass counters and flags come back through pinned memory once, at the end of the frame:
-    // the passes, the resolve and the output copies are queued without a host round trip
-    if (c->host_words < F.npass * F.pass_words + 2) {
-        if (c->host) (void)hipHostFree(c->host);
-        c->host = nullptr;
-        c->host_words = 0;
-        HIP_TRY(hipHostMalloc((void**)&c->host, (size_t)(F.npass * F.pass_words + 2) * 4, hipHostMallocDefault));
-        c->host_words = F.npass * F.pass_words + 2;
-        memset(c->host, 0, (size_t)c->host_words * 4);  // depths beyond used_words stay zero
+    // per-slot buffers of this frame shape (for an asynchronous frame also those of the other slot
+    // while it is idle, so that the pipeline's first frame on it allocates nothing)
+    auto ensure_frame = [&](FrameSlot& fs) -> int {
+        FrameSlot* keep = c->f;
+        c->f = &fs;
+        int r = SRT_OK;
+        if (!r) r = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * npix);
+        if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
+        if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
+        if (!r && a->jitter && !jit_dev) r = ensure_buf(&c->f->jit, c->f->jit_cap, (int64_t)batch * 4 * npix);
+        if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
+        if (!r) r = F.frame ? ensure_ring(c, (int64_t)FRAME_BLOCK * (c->fanout + 2) * 2)
+                            : ensure_queues(c, (int64_t)batch * npix * c->fanout);
+        if (!r && (int)c->f->ev.size() < F.npass * F.nev) {
+            for (hipEvent_t e : c->f->ev) (void)hipEventDestroy(e);
+            c->f->ev.assign(F.npass * F.nev, nullptr);
+            for (auto& e : c->f->ev)
+                if (hipEventCreate(&e) != hipSuccess) r = fail(SRT_ERR_HIP, "hipEventCreate failed");
+        }
+        // per-pass counters and flags come back through pinned memory once, at the end of the
+        // frame: the passes, the resolve and the output copies are queued without a host round trip
+        if (!r && c->f->host_words < F.npass * F.pass_words + 2) {
+            if (c->f->host) (void)hipHostFree(c->f->host);
+            c->f->host = nullptr;
+            c->f->host_words = 0;
+            if (hipHostMalloc((void**)&c->f->host, (size_t)(F.npass * F.pass_words + 2) * 4, hipHostMallocDefault) !=
+                hipSuccess) {
+                r = fail(SRT_ERR_MEMORY, "pinned host allocation failed");
+            } else {
+                c->f->host_words = F.npass * F.pass_words + 2;
+                memset(c->f->host, 0, (size_t)c->f->host_words * 4);  // depths beyond used_words stay zero
+            }
+        }
+        c->f = keep;
+        return r;
+    };
+    if ((rc = ensure_frame(*c->f))) return rc;
+    if (async) {
+        FrameSlot& other = c->slots[(c->f - c->slots) ^ 1];
+        if (other.pending == 0) {
+            if ((rc = ensure_slot(other))) return rc;
+            if ((rc = ensure_frame(other))) return rc;
+        }
     }
     const Variant& V = pick_variant(c->mats);
     // outputs already in device memory are written in place by k_resolve (no copies)
-    double* res_rgb = a->out_rgb ? (rgb_dev ? a->out_rgb : c->rgb) : nullptr;
-    uint8_t* res_u8 = a->out_srgb8 ? (u8_dev ? a->out_srgb8 : c->u8) : nullptr;
+    double* res_rgb = a->out_rgb ? (rgb_dev ? a->out_rgb : c->f->rgb) : nullptr;
+    uint8_t* res_u8 = a->out_srgb8 ? (u8_dev ? a->out_srgb8 : c->f->u8) : nullptr;
     // only the depths this frame can reach are handed back and cleared per pass
     const int64_t used_words = std::min<int64_t>(F.cnt_words, (int64_t)(F.dcap + 2) * NSHARD);
     srt_stats S{};
     for (;;) {
-        if (c->async_pending == 0) clear_host_flags(c, F);  // k_pass_end ORs into them
-        if (c->dirty) {
-            HIP_TRY(hipMemsetAsync(c->shadow, 0, 8 * NSHARD, c->stream));
-            HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)F.cnt_words * 4, c->stream));
-            HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
+        if (c->f->pending == 0) clear_host_flags(c, F);  // k_pass_end ORs into them
+        if (c->f->dirty) {
+            HIP_TRY(hipMemsetAsync(c->f->shadow, 0, 8 * NSHARD, c->f->stream));
+            HIP_TRY(hipMemsetAsync(c->f->counts, 0, (size_t)F.cnt_words * 4, c->f->stream));
+            HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
         }
-        c->dirty = true;
+        c->f->dirty = true;
         for (int p = 0; p < F.npass; ++p) {
             const int s0 = p * batch;
             const int ns = std::min(batch, a->spp - s0);
             const int64_t nrays = (int64_t)ns * npix;
             TraceParams P = base_params(c, a->seed);
-            P.fb = c->fb;
+            P.fb = c->f->fb;
             P.fb_first = (p == 0);  // the first pass's depth-0 kernel stores the framebuffer (no memset)
             // samples per k_primary thread: all of the pass's (accumulated in registers) unless the
             // frame has fewer pixels than a quarter of the resident wave slots, then fewer (pixel x
@@ -1629,7 +1730,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             {
                 const int64_t want_items = (int64_t)c->max_blocks * 64;
                 while (P.spt > 1 && npix * ((ns + P.spt - 1) / P.spt) < want_items) P.spt = (P.spt + 1) / 2;
-                if (P.spt < ns && p == 0) HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * npix * 8, c->stream));
+                if (P.spt < ns && p == 0) HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * npix * 8, c->f->stream));
             }
             P.npix = npix;
             P.cam = *cam;
@@ -1643,99 +1744,103 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 if (jit_dev) {
                     P.jitter = src;
                 } else {
-                    HIP_TRY(hipMemcpyAsync(c->jit, src, (size_t)nrays * 4 * 8, hipMemcpyHostToDevice, c->stream));
-                    P.jitter = c->jit;
+                    HIP_TRY(hipMemcpyAsync(c->f->jit, src, (size_t)nrays * 4 * 8, hipMemcpyHostToDevice, c->f->stream));
+                    P.jitter = c->f->jit;
                 }
             }
-            if (a->out_hit_id) P.hit_out = hit_dev ? a->out_hit_id + (int64_t)s0 * npix : c->hit;
-            hipEvent_t* ev = c->ev.data() + (int64_t)p * F.nev;
+            if (a->out_hit_id) P.hit_out = hit_dev ? a->out_hit_id + (int64_t)s0 * npix : c->f->hit;
+            hipEvent_t* ev = c->f->ev.data() + (int64_t)p * F.nev;
             if (F.frame) {
                 // the whole pass in one launch: one wave per 64-pixel tile
-                P.ring = c->ring;
-                P.ring_lock = c->ring_lock;
-                P.ring_cap = c->ring_cap;
-                P.nslot = c->nslot;
+                P.ring = c->f->ring;
+                P.ring_lock = c->f->ring_lock;
+                P.ring_cap = c->f->ring_cap;
+                P.nslot = c->f->nslot;
                 P.dcap = F.dcap;
-                P.cnt_out = c->counts;
+                P.cnt_out = c->f->counts;
                 P.fuse_resolve = (F.npass == 1);
                 P.out_rgb = res_rgb;
                 P.out_u8 = res_u8;
                 P.spp_total = a->spp;
-                HIP_TRY(hipEventRecord(ev[0], c->stream));
+                HIP_TRY(hipEventRecord(ev[0], c->f->stream));
                 hipLaunchKernelGGL(V.frame, dim3((unsigned)((npix + FRAME_BLOCK - 1) / FRAME_BLOCK)), dim3(FRAME_BLOCK),
-                                   lut_bytes(c), c->stream, P);
+                                   lut_bytes(c), c->f->stream, P);
                 HIP_TRY(hipGetLastError());
-                HIP_TRY(hipEventRecord(ev[1], c->stream));
-                HIP_TRY(hipEventRecord(ev[F.dcap + 1], c->stream));
+                HIP_TRY(hipEventRecord(ev[1], c->f->stream));
+                HIP_TRY(hipEventRecord(ev[F.dcap + 1], c->f->stream));
             } else {
             // depth 0: raygen fused with the trace step
             P.depth = 0;
             P.n_primary = nrays;
-            P.qout = c->q[1];
-            P.cnt_out = c->counts + NSHARD;
-            HIP_TRY(hipEventRecord(ev[0], c->stream));
+            P.qout = c->f->q[1];
+            P.cnt_out = c->f->counts + NSHARD;
+            HIP_TRY(hipEventRecord(ev[0], c->f->stream));
             hipLaunchKernelGGL(V.primary, dim3(grid_for(npix * ((ns + P.spt - 1) / P.spt), c->max_blocks)),
-                               dim3(BLOCK), lut_bytes(c), c->stream, P);
+                               dim3(BLOCK), lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ev[1], c->stream));
+            HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             P.fb_first = 0;
             for (int d = 1; d <= F.dcap; ++d) {
                 if (F.chain_from > 0 && d > F.chain_from) break;  // traced by the chain kernel
                 P.depth = d;
-                P.qin = c->q[d & 1];
-                P.qout = c->q[(d + 1) & 1];
-                P.cnt_in = c->counts + (int64_t)d * NSHARD;
-                P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
+                P.qin = c->f->q[d & 1];
+                P.qout = c->f->q[(d + 1) & 1];
+                P.cnt_in = c->f->counts + (int64_t)d * NSHARD;
+                P.cnt_out = c->f->counts + (int64_t)(d + 1) * NSHARD;
                 P.chain = (d == F.chain_from);
                 P.dcap = F.dcap;
-                hipLaunchKernelGGL(P.chain ? V.chain : V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream,
+                hipLaunchKernelGGL(P.chain ? V.chain : V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream,
                                    P);
                 HIP_TRY(hipGetLastError());
-                HIP_TRY(hipEventRecord(ev[1 + d], c->stream));
+                HIP_TRY(hipEventRecord(ev[1 + d], c->f->stream));
             }
             }
-            uint32_t* hp = c->host + p * F.pass_words;
+            uint32_t* hp = c->f->host + p * F.pass_words;
             // counters of this pass -> pinned host words [0, used_words) (the unused depths are zero
             // on the host), flags OR-ed into the two words at [cnt_words, cnt_words + 2); the last
             // pass's are handed over by k_resolve
             if (p + 1 < F.npass) {
-                hipLaunchKernelGGL(k_pass_end, dim3(1), dim3(BLOCK), 0, c->stream, c->counts, used_words, c->flags,
+                hipLaunchKernelGGL(k_pass_end, dim3(1), dim3(BLOCK), 0, c->f->stream, c->f->counts, used_words, c->f->flags,
                                    hp, hp + F.cnt_words);
                 HIP_TRY(hipGetLastError());
             }
             if (a->out_hit_id && !hit_dev)
-                HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->hit, (size_t)nrays * 4,
-                                       hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->f->hit, (size_t)nrays * 4,
+                                       hipMemcpyDeviceToHost, c->f->stream));
         }
-        uint32_t* hshadow = c->host + F.npass * F.pass_words;
+        uint32_t* hshadow = c->f->host + F.npass * F.pass_words;
         // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
         const bool fused = F.frame && F.npass == 1;
-        uint32_t* hlast = c->host + (F.npass - 1) * F.pass_words;
-        hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->fb,
-                           fused ? (int64_t)0 : npix, c->shadow, hshadow, (double)a->spp, res_rgb, res_u8, c->counts,
-                           used_words, c->flags, hlast, hlast + F.cnt_words);
+        uint32_t* hlast = c->f->host + (F.npass - 1) * F.pass_words;
+        hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
+                           fused ? (int64_t)0 : npix, c->f->shadow, hshadow, (double)a->spp, res_rgb, res_u8, c->f->counts,
+                           used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
-        c->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
+        c->f->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
         if (async) {
-            // stats of this frame (and its errors) come with srt_render_finish
+            // stats of this frame (and its errors) come with srt_render_finish; the next
+            // asynchronous frame goes to the other slot
             c->async_pending++;
-            c->async_plan = F;
+            c->f->pending++;
+            c->f->plan = F;
+            c->last_slot = (int)(c->f - c->slots);
+            c->next_slot = c->last_slot ^ 1;
             return SRT_OK;
         }
         if (a->out_rgb && !rgb_dev)
-            HIP_TRY(hipMemcpyAsync(a->out_rgb, c->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->f->stream));
         if (a->out_srgb8 && !u8_dev)
-            HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->stream));
-        c->dirty = true;
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        c->dirty = false;
+            HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->f->stream));
+        c->f->dirty = true;
+        HIP_TRY(hipStreamSynchronize(c->f->stream));
+        c->f->dirty = false;
         const int64_t retries = S.retries;
         rc = collect_frame(c, F, S);
         if (rc == SRT_RETRY_OVERFLOW) {
             // a queue shard overflowed: grow the queues and render the frame again
             S.retries = retries + 1;
             if (S.retries > 8) return fail(SRT_ERR_MEMORY, "ray queues keep overflowing");
-            if ((rc = F.frame ? ensure_ring(c, 2 * c->ring_cap) : ensure_queues(c, 2 * c->seg * NSHARD))) return rc;
+            if ((rc = F.frame ? ensure_ring(c, 2 * c->f->ring_cap) : ensure_queues(c, 2 * c->f->seg * NSHARD))) return rc;
             continue;
         }
         S.retries = retries;
@@ -1757,7 +1862,7 @@ int srt_render_finish(srt_ctx* c, srt_stats* st) {
 
 int srt_stream(srt_ctx* c, void** stream) {
     if (!c || !stream) return fail(SRT_ERR_ARG, "null argument");
-    *stream = (void*)c->stream;
+    *stream = (void*)c->f->stream;
     return SRT_OK;
 }
 
@@ -1771,7 +1876,7 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
     HIP_TRY(hipSetDevice(c->device));
     int rc0 = finish_async(c, nullptr);
     if (rc0) return rc0;
-    c->dirty = true;  // counts/flags/shadow are left as this call's memsets and kernels leave them
+    c->f->dirty = true;  // counts/flags/shadow are left as this call's memsets and kernels leave them
     const int64_t n = a->n;
     int rc = SRT_OK;
     double *O = nullptr, *D = nullptr;
@@ -1779,10 +1884,10 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
     HIP_TRY(dalloc(&O, 3 * n));
     HIP_TRY(dalloc(&D, 3 * n));
     if (a->medium) HIP_TRY(dalloc(&med, n));
-    HIP_TRY(hipMemcpyAsync(O, a->origin, (size_t)3 * n * 8, hipMemcpyDefault, c->stream));
-    HIP_TRY(hipMemcpyAsync(D, a->dir, (size_t)3 * n * 8, hipMemcpyDefault, c->stream));
-    if (med) HIP_TRY(hipMemcpyAsync(med, a->medium, (size_t)n * 4, hipMemcpyDefault, c->stream));
-    if ((rc = ensure_buf(&c->fb, c->fb_cap, 3 * n))) return rc;
+    HIP_TRY(hipMemcpyAsync(O, a->origin, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
+    HIP_TRY(hipMemcpyAsync(D, a->dir, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
+    if (med) HIP_TRY(hipMemcpyAsync(med, a->medium, (size_t)n * 4, hipMemcpyDefault, c->f->stream));
+    if ((rc = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * n))) return rc;
     if ((rc = ensure_queues(c, n * c->fanout))) return rc;
     // depths a->depth .. a->depth + cap (the batch's depth is a scalar in the reference)
     const int d0 = a->depth;
@@ -1791,51 +1896,51 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
     std::vector<uint32_t> counts(SRT_MAX_DEPTHS * NSHARD);
     for (int attempt = 0;; ++attempt) {
         if (attempt > 8) { rc = fail(SRT_ERR_MEMORY, "ray queues keep overflowing"); break; }
-        HIP_TRY(hipMemsetAsync(c->fb, 0, (size_t)3 * n * 8, c->stream));
-        HIP_TRY(hipMemsetAsync(c->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->stream));
-        HIP_TRY(hipMemsetAsync(c->flags, 0, 8, c->stream));
-        HIP_TRY(hipMemsetAsync(c->shadow, 0, 8 * NSHARD, c->stream));
+        HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * n * 8, c->f->stream));
+        HIP_TRY(hipMemsetAsync(c->f->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->f->stream));
+        HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
+        HIP_TRY(hipMemsetAsync(c->f->shadow, 0, 8 * NSHARD, c->f->stream));
         uint32_t seed_counts[NSHARD];
         for (int s = 0; s < NSHARD; ++s) seed_counts[s] = (uint32_t)((n - s + NSHARD - 1) / NSHARD);
-        HIP_TRY(hipMemcpyAsync(c->counts + (int64_t)d0 * NSHARD, seed_counts, sizeof(seed_counts),
-                               hipMemcpyHostToDevice, c->stream));
-        hipLaunchKernelGGL(k_seed_queue, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->q[d0 & 1],
-                           c->seg, O, D, med, n, (uint32_t)d0, (uint32_t)a->diffuse_reflections, (uint32_t)c->S.nmedia);
+        HIP_TRY(hipMemcpyAsync(c->f->counts + (int64_t)d0 * NSHARD, seed_counts, sizeof(seed_counts),
+                               hipMemcpyHostToDevice, c->f->stream));
+        hipLaunchKernelGGL(k_seed_queue, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->q[d0 & 1],
+                           c->f->seg, O, D, med, n, (uint32_t)d0, (uint32_t)a->diffuse_reflections, (uint32_t)c->S.nmedia);
         HIP_TRY(hipGetLastError());
         TraceParams P = base_params(c, a->seed);
-        P.fb = c->fb;
+        P.fb = c->f->fb;
         P.npix = n;
         const Variant& V = pick_variant(c->mats);
         for (int d = d0; d <= dlast; ++d) {
             P.depth = d;
-            P.qin = c->q[d & 1];
-            P.qout = c->q[(d + 1) & 1];
-            P.cnt_in = c->counts + (int64_t)d * NSHARD;
-            P.cnt_out = c->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->stream, P);
+            P.qin = c->f->q[d & 1];
+            P.qout = c->f->q[(d + 1) & 1];
+            P.cnt_in = c->f->counts + (int64_t)d * NSHARD;
+            P.cnt_out = c->f->counts + (int64_t)(d + 1) * NSHARD;
+            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
         }
         uint32_t flags[2];
         unsigned long long shadow = 0;
-        HIP_TRY(hipMemcpyAsync(counts.data(), c->counts, counts.size() * 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(flags, c->flags, sizeof(flags), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(&shadow, c->shadow, 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpyAsync(counts.data(), c->f->counts, counts.size() * 4, hipMemcpyDeviceToHost, c->f->stream));
+        HIP_TRY(hipMemcpyAsync(flags, c->f->flags, sizeof(flags), hipMemcpyDeviceToHost, c->f->stream));
+        HIP_TRY(hipMemcpyAsync(&shadow, c->f->shadow, 8, hipMemcpyDeviceToHost, c->f->stream));
+        HIP_TRY(hipStreamSynchronize(c->f->stream));
         if ((rc = check_flags(flags[0]))) break;
         if (flags[1]) {
             S.retries++;
-            if ((rc = ensure_queues(c, 2 * c->seg * NSHARD))) break;
+            if ((rc = ensure_queues(c, 2 * c->f->seg * NSHARD))) break;
             continue;
         }
-        if (depth_total(counts.data() + (int64_t)(dlast + 1) * NSHARD, c->seg) != 0) {
+        if (depth_total(counts.data() + (int64_t)(dlast + 1) * NSHARD, c->f->seg) != 0) {
             rc = fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
             break;
         }
-        for (int d = d0; d <= dlast; ++d) S.rays_per_depth[d] = depth_total(counts.data() + (int64_t)d * NSHARD, c->seg);
+        for (int d = d0; d <= dlast; ++d) S.rays_per_depth[d] = depth_total(counts.data() + (int64_t)d * NSHARD, c->f->seg);
         S.n_depths = dlast + 1;
         for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.total_rays += S.rays_per_depth[d];
         S.shadow_rays = (int64_t)shadow;
-        HIP_TRY(hipMemcpy(a->out_rgb, c->fb, (size_t)3 * n * 8, hipMemcpyDefault));
+        HIP_TRY(hipMemcpy(a->out_rgb, c->f->fb, (size_t)3 * n * 8, hipMemcpyDefault));
         break;
     }
     (void)hipFree(O);
@@ -1861,10 +1966,10 @@ int srt_nearest(srt_ctx* c, const double* O, const double* D, int64_t n, double*
     HIP_TRY(dalloc(&did, n));
     HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
-    hipLaunchKernelGGL(k_nearest, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, c->S, dO, dD, n, dt, did,
+    hipLaunchKernelGGL(k_nearest, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->S, dO, dD, n, dt, did,
                        dor);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
     if (t) HIP_TRY(hipMemcpy(t, dt, (size_t)n * 8, hipMemcpyDefault));
     if (id) HIP_TRY(hipMemcpy(id, did, (size_t)n * 4, hipMemcpyDefault));
     if (orient) HIP_TRY(hipMemcpy(orient, dor, (size_t)n * 8, hipMemcpyDefault));
@@ -1888,10 +1993,10 @@ int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O,
     HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dcol, col, sizeof(srt_collider), hipMemcpyDefault));
-    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, dcol, dO, dD, n,
+    hipLaunchKernelGGL(k_intersect_one, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, dcol, dO, dD, n,
                        dout);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
     HIP_TRY(hipMemcpy(out, dout, (size_t)2 * n * 8, hipMemcpyDefault));
     (void)hipFree(dcol);
     (void)hipFree(dO);
@@ -1916,9 +2021,9 @@ int srt_primary_rays(srt_ctx* c, const srt_camera* cam, const double* J, double*
     srt_camera k = *cam;
     k.xs = xs;
     k.ys = ys;
-    hipLaunchKernelGGL(k_primary_rays, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->stream, k, dJ, n, dO, dD);
+    hipLaunchKernelGGL(k_primary_rays, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, k, dJ, n, dO, dD);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
     HIP_TRY(hipMemcpy(O, dO, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(D, dD, (size_t)3 * n * 8, hipMemcpyDefault));
     void* bufs[] = {dJ, dO, dD, xs, ys};
@@ -1961,7 +2066,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     constexpr int64_t NTAB = 31 * rtmt::N;
     if (!c->mt) {
         HIP_TRY(dalloc(&c->mt, NTAB + 3 * rtmt::N));
-        HIP_TRY(hipMemcpyAsync(c->mt, rtmt::tables_flat(), NTAB * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->mt, rtmt::tables_flat(), NTAB * 4, hipMemcpyHostToDevice, c->f->stream));
     }
     uint32_t* keys[2] = {c->mt + NTAB, c->mt + NTAB + rtmt::N};
     uint32_t* dump = c->mt + NTAB + 2 * rtmt::N;
@@ -1972,7 +2077,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
         if (rc) return rc;
         dst = c->mt_out;
     }
-    HIP_TRY(hipMemcpyAsync(keys[0], key, rtmt::N * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(keys[0], key, rtmt::N * 4, hipMemcpyHostToDevice, c->f->stream));
     const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
     for (size_t r = 0; r < plan.rounds.size(); ++r) {
         const rtmt::Round& R = plan.rounds[r];
@@ -1987,12 +2092,12 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
         A.n_out = n_out;
         A.dump_at = R.dump_at;
         A.pos = R.pos;
-        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), 0, c->stream, A);
+        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), 0, c->f->stream, A);
         HIP_TRY(hipGetLastError());
     }
-    if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(key_out, dump, rtmt::N * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, c->f->stream));
+    HIP_TRY(hipMemcpyAsync(key_out, dump, rtmt::N * 4, hipMemcpyDeviceToHost, c->f->stream));
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
     *pos_out = plan.final_pos;
     return SRT_OK;
 }
@@ -2002,7 +2107,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
 int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
     if (!c || !out) return fail(SRT_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_prof), sizeof(unsigned long long) * 64));
     if (reset) {
         unsigned long long z[64] = {};
@@ -2015,7 +2120,8 @@ int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
 int srt_synchronize(srt_ctx* c) {
     if (!c) return fail(SRT_ERR_ARG, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (FrameSlot& f : c->slots)
+        if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
     return SRT_OK;
 }
 
