@@ -147,6 +147,9 @@ def main():
     lib, ctx = B.context()
     if args.occupancy:
         N.check(lib, lib.srt_set_option(ctx, b"occupancy", args.occupancy))
+    if not args.sync:
+        # size every frame slot during the warmup (the first pipelined frame would allocate them)
+        N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))
     for kv in args.option:
         k, v = kv.split("=")
         N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
@@ -196,12 +199,13 @@ def main():
     # place by k_resolve, double-buffered) is all-gathered over RCCL on torch's stream after the
     # frame, overlapping the next frame's rendering.
     pipelined = not args.sync and args.rng != "mt"
-    tiles, done = None, [None, None]
+    NTILE = 3  # frames in flight (library frame slots) + 1
+    tiles, done = None, [None] * NTILE
     if dist is not None:
         import torch
 
         # each rank's uint8 tile, padded to the largest shard: the send buffer of the all-gather
-        tiles = [torch.zeros((max_shard_rows(H, world), W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        tiles = [torch.zeros((max_shard_rows(H, world), W, 3), dtype=torch.uint8, device="cuda") for _ in range(NTILE)]
         gather = RowGather(H, world, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
     streams = {}
 
@@ -223,13 +227,13 @@ def main():
             # the reference's stream (seed 0): spp x 4 x npix jitter + the sizing draw, on the GPU
             N.check(lib, lib.srt_mt19937_uniforms(ctx, N.ptr(mt_key), int(mt_state[2]), spp * 4 * npix, 4 * npix,
                                                   jit_dev, N.ptr(mt_key_out), ctypes.byref(mt_pos_out)))
-        i = frame["k"] % 2
+        i = frame["k"] % NTILE
         frame["k"] += 1
         a.flags = N.RENDER_ASYNC if (pipelined and async_ok) else 0
         if tiles is not None:
             if done[i] is not None:
-                # the gather that read this tile two frames ago must be done before this frame's
-                # resolve overwrites it (a host wait: two frames later it has long finished)
+                # the gather that read this tile NTILE frames ago must be done before this frame's
+                # resolve overwrites it (a host wait: by now it has long finished)
                 done[i].synchronize()
             a.out_srgb8 = ctypes.c_void_p(tiles[i].data_ptr())
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))

@@ -246,7 +246,8 @@ int srt_device_count(int* count);
 int srt_create(int device, srt_ctx** out);
 int srt_destroy(srt_ctx* ctx);
 /* options: "queue_bytes" (HBM budget for ray queues), "bvh" (0: no triangle BVH), "max_blocks" (grid cap of the wavefront
- * kernels), "frame_kernel" (-1 auto = frame kernel for branching scenes, 0 per-depth wavefront
+ * kernels), "pipeline" (1: size every frame slot on each render, so the first pipelined frame
+ * allocates nothing), "frame_kernel" (-1 auto = frame kernel for branching scenes, 0 per-depth wavefront
  * kernels, 1 frame kernel), "occupancy" (experiment: waves/SIMD bound of the ex1 variant) */
 int srt_set_option(srt_ctx* ctx, const char* key, int64_t value);
 int srt_upload_scene(srt_ctx* ctx, const srt_scene_desc* scene);
