@@ -24,6 +24,7 @@ for step in "$@"; do
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench_sync) run bench_sync 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sync ;;
+    prof_sync) run prof_sync 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sync -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sync ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
