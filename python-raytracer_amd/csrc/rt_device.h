@@ -368,15 +368,15 @@ RT_HD d3 collider_normal(const RT_RO srt_collider& c, d3 P) {
 }
 
 // cuboid.py:153-187: 4x3 cube-cross coordinates; every face divides by `width`
-RT_HD double cross_coord(d3 ax, double sgn, d3 MC, double width, double shift) {
+RT_HD double cross_coord(d3 ax, double sgn, d3 MC, const Quot& width, double shift) {
     d3 a = d3{ax.x * sgn, ax.y * sgn, ax.z * sgn};
-    return ((((dot(a, MC) / width) * 2.0) * 0.985 + 1.0) / 2.0) + shift;
+    return (((width(dot(a, MC)) * 2.0) * 0.985 + 1.0) / 2.0) + shift;
 }
 RT_HD void cuboid_uv(const RT_RO double* p, d3 P, double& u, double& v) {
     d3 N = cuboid_normal(p, P);
     d3 MC = sub(P, ld3(p));
     d3 aw = ld3(p + 18), ah = ld3(p + 21), al = ld3(p + 24);
-    double w = p[27];
+    const Quot w(p[27]);  // both coordinates divide by the width
     if (N.x == 0.0 && N.y == -1.0 && N.z == 0.0) {  // BOTTOM
         u = cross_coord(aw, 1.0, MC, w, 1.0); v = cross_coord(al, -1.0, MC, w, 0.0);
     } else if (N.x == 0.0 && N.y == 1.0 && N.z == 0.0) {  // TOP
@@ -413,8 +413,8 @@ RT_HD bool collider_uv(const RT_RO srt_collider& c, d3 P, double& u, double& v) 
         default: u = 0.0; v = 0.0; return false;
     }
     if (c.flags & SRT_CF_UV_CROSS) {  // cuboid.py:29-32, skybox.py:29-32
-        u = u / 4.0;
-        v = v / 3.0;
+        u = u / 4.0;  // exact: a multiplication by 0.25
+        v = Quot(3.0)(v);
     }
     return true;
 }
@@ -522,9 +522,11 @@ struct Ray {
 };
 
 // Camera.get_ray for one pixel (camera.py:51-85, utils/random.py:6-9)
-RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double j[4], d3& O, d3& D) {
-    double x = xc + ((j[0] - 0.5) * cam.cam_width) / (double)cam.width;
-    double y = yr + ((j[1] - 0.5) * cam.cam_height) / (double)cam.height;
+// qw, qh: the divisions by the screen size (Quot: the kernels build them once per thread)
+RT_HD void primary_ray(const srt_camera& cam, const Quot& qw, const Quot& qh, double xc, double yr,
+                       const double j[4], d3& O, d3& D) {
+    double x = xc + qw((j[0] - 0.5) * cam.cam_width);
+    double y = yr + qh((j[1] - 0.5) * cam.cam_height);
     // pinhole (lens_radius == 0, every example): the disk offsets are (r cos, r sin) * 0 = +-0 and
     // leave O = look_from, so the sqrt/sincos of the disk sample are skipped (0 stands in for them)
     double rx = 0.0, ry = 0.0;
@@ -539,6 +541,9 @@ RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double
     d3 t = add(add(add(lf, mul(mul(U, y), cam.focal_distance)), mul(mul(R, x), cam.focal_distance)),
                ld3(cam.fwd_fd));
     D = normalize(sub(t, O));
+}
+RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double j[4], d3& O, d3& D) {
+    primary_ray(cam, Quot((double)cam.width), Quot((double)cam.height), xc, yr, j, O, D);
 }
 
 // Nearest collider over the scene (ray.py:124-132): nearest = reduce(np.minimum, distances);

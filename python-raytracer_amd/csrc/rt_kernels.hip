@@ -326,6 +326,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     uint32_t shadow = 0;
     const int64_t ngroups = (P.spp + P.spt - 1) / P.spt;
     const int64_t n = P.npix * ngroups;
+    const Quot qw((double)P.cam.width), qh((double)P.cam.height);
     for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
         const int64_t i = base + threadIdx.x;
         const bool active = i < n;
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
             RT_T0(tr0);
             if (active && s + 1 < s_end) primary_uniforms(P, s + 1, p, gpix, jn);
-            if (active) primary_ray(P.cam, xc, yr, j, r.o, r.d);
+            if (active) primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
             RT_ACC(0, tr0);
             int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
             RT_T0(tt0);
@@ -593,6 +594,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     const int grow = pact ? P.rows[lr] : 0;
     const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
     const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
+    const Quot qw((double)P.cam.width), qh((double)P.cam.height);
     int s_next = 0;
     for (;;) {
         const uint32_t head = lds_get(&L.head), tail = lds_get(&L.tail);
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             if (active) {
                 double j[4];
                 primary_uniforms(P, s, p, gpix, j);
-                primary_ray(P.cam, xc, yr, j, r.o, r.d);
+                primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
             }
             RT_ACC(15, tg0);
             if (P.hit_out && active) hs = P.hit_out + (int64_t)s * P.npix + p;
