@@ -322,3 +322,48 @@ def test_gpu_create_animation_frames(tmp_path, monkeypatch):
         got = np.array(Image.open(tmp_path / "frames" / ("anim_%d.png" % i)))
         assert np.array_equal(got, ref), i
         t += 1.0 / 3
+
+
+@pytest.mark.parametrize("mode", ["wavefront", "frame"])
+@pytest.mark.parametrize("shape", [(1, 1), (67, 13), (13, 67), (129, 3)])
+def test_gpu_edge_shapes_match_oracle(shape, mode):
+    """Frame shapes that leave partial waves / blocks / tiles everywhere (1x1, odd sizes) through
+    both trace strategies, against the oracle on the same jitter."""
+    W, H = shape
+    sc = scenes.example1(W, H, 3)
+    np.random.seed(2)
+    jit = sc.camera.draw_jitter(3)
+    _set_option("frame_kernel", 1 if mode == "frame" else 0)
+    try:
+        out = _backend().render_scene(sc, 3, jitter=jit, seed=1, want_hits=True)
+    finally:
+        _set_option("frame_kernel", -1)
+    rgb, ids, counts = O.render_linear(sc, jit)
+    assert np.array_equal(out.hit_ids, ids)
+    assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+    np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("which", ["no_background", "background_only"])
+def test_gpu_degenerate_scenes(which):
+    """Rays that miss everything (no SkyBox: black, ray.py:134-146) and a scene with nothing but the
+    background."""
+    from sightpy import Scene, rgb as RGB, vec3
+
+    if which == "no_background":
+        sc = scenes.example1(40, 30, 3)
+        sc.collider_list = [c for c in sc.collider_list if type(c.assigned_primitive).__name__ != "SkyBox"]
+        sc.scene_primitives = [p for p in sc.scene_primitives if type(p).__name__ != "SkyBox"]
+    else:
+        sc = Scene(ambient_color=RGB(0.05, 0.05, 0.05))
+        sc.add_Camera(look_from=vec3(0.0, 0.25, 1.0), look_at=vec3(0.0, 0.25, -3.0), screen_width=40,
+                      screen_height=30)
+        sc.add_Background("stormydays.png")
+    np.random.seed(6)
+    jit = sc.camera.draw_jitter(2)
+    out = _backend().render_scene(sc, 2, jitter=jit, seed=1, want_hits=True)
+    rgb, ids, counts = O.render_linear(sc, jit)
+    assert np.array_equal(out.hit_ids, ids)
+    np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
+    if which == "no_background":
+        assert (ids == -1).any()
