@@ -116,6 +116,10 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job, to size the per-rank work "
                          "of the multi-GPU run without the gather")
+    ap.add_argument("--rehearse-gather", action="store_true",
+                    help="diagnostic (1 GPU, with --shard-of N): run the N-rank step as one rank would, including "
+                         "the per-frame RCCL all-gather call (a 1-rank group) and row assembly, to size the host "
+                         "and stream overhead of the multi-GPU step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,7 +131,12 @@ def main():
     backend = os.environ.get("SIGHTPY_BENCH_BACKEND", "nccl")
     os.environ.setdefault("SIGHTPY_DEVICE", str(dev))
     dist = None
-    if world > 1:
+    if args.rehearse_gather and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or args.rehearse_gather:
         import torch
         import torch.distributed as dist
 
@@ -207,6 +216,9 @@ def main():
         # each rank's uint8 tile, padded to the largest shard: the send buffer of the all-gather
         tiles = [torch.zeros((max_shard_rows(H, world), W, 3), dtype=torch.uint8, device="cuda") for _ in range(NTILE)]
         gather = RowGather(H, world, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
+        if world == 1:  # --rehearse-gather: rank 0's tile of an N-rank job through a 1-rank group
+            tiles = [torch.zeros((len(rows), W, 3), dtype=torch.uint8, device="cuda") for _ in range(NTILE)]
+            gather = RowGather(len(rows), 1, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
     streams = {}
 
     def frame_stream():
@@ -324,7 +336,9 @@ def main():
                        "rays_per_frame": int(total_rays), "rays_per_depth_rank0": rpd,
                        "shadow_rays_rank0": stats[0]["shadow_rays"], "kernel_path": stats[0]["kernel_path"],
                        "chain_from_depth": stats[0]["chain_from"], "parallelism": ("row-band shards x%d" % world) if not args.shard_of
-                       else "diagnostic: rank 0 of %d row-band shards, no gather" % args.shard_of,
+                       else "diagnostic: rank 0 of %d row-band shards, %s" % (
+                           args.shard_of, "1-rank RCCL all-gather + assembly per frame" if args.rehearse_gather
+                           else "no gather"),
                        "frame_ms": round(ms_step, 4)},
             "roofline": {"bound": "hbm",
                          "kernel": "k_frame (whole pass: every ray of every depth, one wave per 64-pixel tile)"

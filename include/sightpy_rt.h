@@ -113,7 +113,9 @@ typedef struct srt_material {
     int32_t normalmap; /* normal-map texture, -1 = none */
     int32_t medium;    /* REFRACTIVE: media[] row holding its n */
     uint32_t flags;    /* SRT_MF_* */
-    int32_t ival;      /* DIFFUSE: diffuse_rays */
+    int32_t ival;      /* DIFFUSE: diffuse_rays; GLOSSY: k > 0 when the lobe exponent p[4] is within
+                          4 ulp of the integer k (x^p[4] is then evaluated as x^k, < 1e-12 relative
+                          apart), 0 = general pow */
     double p[SRT_MATERIAL_PARAMS];
 } srt_material;
 

@@ -7,6 +7,8 @@ bit-identical constants.  Per-medium quantities (the specular F0 depends on the 
 refraction) are tabulated over the finite set of media a ray can be in: scene.n and the n of
 every Refractive material.
 """
+import os
+
 import numpy as np
 
 from . import _native as N
@@ -287,6 +289,9 @@ def lower_scene(scene, extra_media=()):
                 a = 2.0 / (m.roughness ** 2.0) - 2.0
                 p[4] = a
                 p[5] = a + 2.0
+                k = int(round(a))
+                if 1 <= k <= 1 << 20 and abs(a - k) <= 4.0 * np.spacing(a) and not os.environ.get("SIGHTPY_NO_POWI"):
+                    r["ival"] = k  # device evaluates x**a as x**k (rt_device.h powi)
             p[6] = 2.0 * np.pi
             p[7] = m.spec_coeff
             F0 = np.abs((scene.n - m.n) / (scene.n + m.n)) ** 2  # glossy.py:91 (Python scalars)

@@ -62,3 +62,23 @@ def test_texel_pool_persists_across_lowerings():
     floor.diff_texture = image("wood.jpg", repeat=80.0)
     c = lower_scene(sc)
     assert c.texel_key != a.texel_key and c.texels.size != a.texels.size
+
+
+def test_glossy_integer_lobe_exponent():
+    """Glossy lobe exponent a = 2/roughness^2 - 2 (glossy.py:71): lowered with an integer k in
+    `ival` only when a is within 4 ulp of k (roughness 0.2 -> 47.99999999999999 -> 48, 0.5 -> 6),
+    otherwise the device keeps pow (0.3 -> 20.22..., 0.15 -> 86.88...)."""
+    from sightpy._lower import lower_scene
+    from sightpy import _native as N
+
+    L = lower_scene(scenes.features(16, 12))
+    seen = {}
+    for r in L.materials:
+        if r["type"] == N.GLOSSY and r["flags"] & N.MF_ROUGH:
+            a = float(r["p"][4])
+            seen[round(a, 6)] = int(r["ival"])
+            if r["ival"]:
+                assert abs(a - r["ival"]) <= 4 * np.spacing(a)
+                x = np.linspace(0.0, 1.0, 1001)
+                np.testing.assert_allclose(x ** r["ival"], x ** a, rtol=1e-12, atol=1e-300)
+    assert seen[6.0] == 6 and seen[round(2 / 0.3 ** 2 - 2, 6)] == 0
