@@ -208,7 +208,7 @@ def main():
     # place by k_resolve, double-buffered) is all-gathered over RCCL on torch's stream after the
     # frame, overlapping the next frame's rendering.
     pipelined = not args.sync and args.rng != "mt"
-    NTILE = 3  # frames in flight (library frame slots) + 1
+    NTILE = int(os.environ.get("SIGHTPY_BENCH_NTILE", "5"))  # uint8 tiles in flight (gather ring)
     tiles, done = None, [None] * NTILE
     if dist is not None:
         import torch

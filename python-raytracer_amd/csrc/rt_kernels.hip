@@ -218,7 +218,9 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
                                                  double j[4]) {
     if (P.jitter) {
         const double* base = P.jitter + (int64_t)s * 4 * P.npix + p;
-        j[0] = base[0]; j[1] = base[P.npix]; j[2] = base[2 * P.npix]; j[3] = base[3 * P.npix];
+        j[0] = base[0]; j[1] = base[P.npix];
+        // the lens-disk pair is read only by a thin-lens camera (pinhole: primary_ray skips it)
+        if (P.cam.lens_radius != 0.0) { j[2] = base[2 * P.npix]; j[3] = base[3 * P.npix]; }
     } else {
         Rng g;
         g.init(P.seed, gpix, (uint32_t)(P.sample_base + s), 0xCA3E0000u);
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
             RT_T0(tg0);
             if (active) {
-                double j[4];
+                double j[4] = {0.0, 0.0, 0.0, 0.0};
                 primary_uniforms(P, s, p, gpix, j);
                 primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
             }
