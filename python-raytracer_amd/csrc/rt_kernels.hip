@@ -749,16 +749,20 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npi
             flags[threadIdx.x] = 0u;
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
         // the frame's shadow-ray count (NSHARD counters) to the host, zeroed for the next frame (no
-        // kernel of this frame adds to them any more)
+        // kernel of this frame adds to them any more): wave 0 reads them in parallel and reduces
+        // across lanes
         unsigned long long v = 0;
-        for (int k = 0; k < NSHARD; ++k) {
+        for (int k = threadIdx.x; k < NSHARD; k += 64) {
             v += shadow[k];
             shadow[k] = 0ull;
         }
-        shadow_host[0] = (uint32_t)v;
-        shadow_host[1] = (uint32_t)(v >> 32);
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (threadIdx.x == 0) {
+            shadow_host[0] = (uint32_t)v;
+            shadow_host[1] = (uint32_t)(v >> 32);
+        }
     }
     for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK) {
         double r = fb[p] / spp, g = fb[npix + p] / spp, b = fb[2 * npix + p] / spp;
