@@ -82,8 +82,9 @@ class Scene:
         elif rng != "device":
             raise ValueError("rng must be 'numpy', 'numpy-host' or 'device'")
         if world == 1:
+            # only the uint8 image leaves the GPU (the linear RGB stays there: 8x fewer PCIe bytes)
             out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size,
-                               jitter_device=jitter_dev)
+                               jitter_device=jitter_dev, want_rgb=False)
             srgb8 = out.srgb8
         else:
             # one process per GPU under torch.distributed: render this rank's row bands, gather
@@ -94,7 +95,8 @@ class Scene:
             rows = shard_rows(H, world, rank)
             if jitter is not None:
                 jitter = jitter.reshape(samples_per_pixel, 4, H, W)[:, :, rows].reshape(samples_per_pixel, 4, -1)
-            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size, rows=rows)
+            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size, rows=rows,
+                               want_rgb=False)
             tile = torch.from_numpy(out.srgb8)
             if torch.distributed.get_backend() == "nccl":
                 tile = tile.cuda()

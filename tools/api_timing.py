@@ -1,0 +1,59 @@
+"""End-to-end rate of the public API: `Scene.render(spp)` exactly as an example script calls it
+(scene.py:60-104 here, reference scene.py:71-140): the reference's numpy jitter stream generated on
+the GPU, every sample and depth traced, the linear RGB (f64) and uint8 image copied to host memory
+over PCIe, and the PIL image built.  This is the host-buffer rate DESIGN.md §5 quotes next to
+bench.py's device-resident `value`.
+
+    python tools/api_timing.py [--config example1_1080p_d5] [--repeats 5]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+for p in (ROOT / "python-raytracer_amd", ROOT / "tests", ROOT):
+    sys.path.insert(0, str(p))
+
+
+def main():
+    import numpy as np
+    import scenes
+    from bench import CONFIGS
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
+    ap.add_argument("--repeats", type=int, default=5)
+    ap.add_argument("--profile", action="store_true", help="cProfile one render (host-side breakdown)")
+    a = ap.parse_args()
+    builder, W, H, depth, spp, label = CONFIGS[a.config]
+    sc = getattr(scenes, builder)(W, H, depth)
+    np.random.seed(0)
+    sc.render(spp)  # warmup: scene upload, queue sizing
+    times = []
+    for _ in range(a.repeats):
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        img = sc.render(spp)
+        times.append(time.perf_counter() - t0)
+    if a.profile:
+        import cProfile
+        import pstats
+
+        np.random.seed(0)
+        pr = cProfile.Profile()
+        pr.enable()
+        sc.render(spp)
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(25)
+    rays = sc.last_stats["total_rays"]
+    best, med = min(times), float(np.median(times))
+    print(json.dumps({"what": "Scene.render(%d) via the public API, host buffers (PCIe-inclusive)" % spp,
+                      "workload": label, "image": list(img.size), "rays_per_frame": int(rays),
+                      "ms_median": round(med * 1e3, 3), "ms_min": round(best * 1e3, 3),
+                      "Mrays_per_s_median": round(rays / med / 1e6, 1), "repeats": a.repeats}))
+
+
+if __name__ == "__main__":
+    main()
