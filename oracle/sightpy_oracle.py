@@ -15,7 +15,16 @@ scalar-vec3-times-array expressions element for element.
 
 Pinned against the reference itself: tests/golden/*.npz were produced by importing the reference
 in the build container (tests/golden/gen_golden.py); tests/test_oracle.py checks this module
-against them (bit-exact for geometry, <=1e-12 relative for colours).
+against them (bit-exact for geometry, <=1e-12 relative for colours), Monte-Carlo scenes included
+(single-process seeded renders of the reference are deterministic).
+
+Random numbers.  By default every draw comes from numpy's global RNG in the reference's order
+(camera jitter, `mixed_pdf`/`cosine_pdf`/`spherical_caps_pdf` draws, the `mc=True` pick), which is
+what pins this module to the reference.  With `rng=DeviceStream(seed)` the Monte-Carlo draws
+instead come from the device's counter-based stream -- Philox4x32-10 keyed by (seed, global pixel,
+child-path hash, tag), restated here from csrc/rt_device.h and rt_kernels.hip -- so the GPU's
+Monte-Carlo paths can be compared with this restatement sample for sample (tests/test_gpu_mc.py).
+The algorithm code is the same in both modes; only the source of the uniforms differs.
 """
 import numpy as np
 
@@ -57,20 +66,106 @@ def texel(img, u, v, rep, shape=None):
     return img[-((v * h * rep).astype(int) % h), (u * w * rep).astype(int) % w].T
 
 
-class Rays:
-    """A batch: origin/dir (3, n), medium index n (3, n) or (3, 1), batch-scalar counters."""
+# ---- the device's counter-based stream (csrc/rt_device.h Rng / philox / mix32) -----------------
+_M32 = 0xFFFFFFFF
 
-    def __init__(self, O, D, n, depth, diffuse_reflections=0):
+
+def mix32(h, v):
+    """rt_device.h mix32 on uint32 arrays."""
+    h = np.asarray(h).astype(np.uint64)
+    v = np.asarray(v).astype(np.uint64)
+    h = h ^ ((v + 0x9E3779B9 + ((h << np.uint64(6)) & _M32) + (h >> np.uint64(2))) & _M32)
+    h = (h * 0x85EBCA6B) & _M32
+    return (h ^ (h >> np.uint64(13))).astype(np.uint32)
+
+
+def child_path(path, slot, rnd):
+    """rt_device.h child_path: the RNG identity of a child ray (slot, tie round)."""
+    return mix32(path, (np.asarray(slot).astype(np.uint64) + 4096 * np.asarray(rnd).astype(np.uint64)) & _M32)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 (Salmon et al., SC'11), as rt_device.h philox: four uint32 counter words."""
+    a, b, c, d = (np.asarray(x).astype(np.uint64) for x in (c0, c1, c2, c3))
+    k0, k1 = np.uint64(k0), np.uint64(k1)
+    for _ in range(10):
+        p0 = a * np.uint64(0xD2511F53)
+        p1 = c * np.uint64(0xCD9E8D57)
+        a, b, c, d = (p1 >> np.uint64(32)) ^ b ^ k0, p1 & _M32, (p0 >> np.uint64(32)) ^ d ^ k1, p0 & _M32
+        k0 = (k0 + np.uint64(0x9E3779B9)) & np.uint64(_M32)
+        k1 = (k1 + np.uint64(0xBB67AE85)) & np.uint64(_M32)
+    return a, b, c, d
+
+
+def u01(a, b):
+    """numpy's 53-bit double from two 32-bit words (rt_device.h u01)."""
+    return ((a >> np.uint64(5)).astype(np.float64) * 67108864.0 + (b >> np.uint64(6)).astype(np.float64)) / 9007199254740992.0
+
+
+class DeviceStream:
+    """The uniforms the GPU draws for its Monte-Carlo shading: Rng.init(seed, pix, path, tag), call n
+    returns the pair (u01(r.a, r.b), u01(r.c, r.d)) of philox((pix, path, tag, n), seed)."""
+
+    def __init__(self, seed):
+        seed = int(seed) & (2**64 - 1)
+        self.k0, self.k1 = seed & _M32, seed >> 32
+
+    def pair(self, pix, path, tag, n):
+        size = np.broadcast(np.asarray(pix), np.asarray(path), np.asarray(tag)).shape
+        a, b, c, d = philox4x32_10(np.broadcast_to(pix, size), np.broadcast_to(path, size),
+                                   np.broadcast_to(tag, size), np.full(size, n), self.k0, self.k1)
+        return u01(a, b), u01(c, d)
+
+
+    def jitter(self, npix, spp, sample_base=0):
+        """The camera uniforms of the device-RNG render mode (render jitter NULL; rt_kernels.hip
+        primary_uniforms): pixel p, sample s -> pairs 0, 1 of Rng(seed, p, sample_base + s, TAG_RAYGEN)."""
+        pix = np.arange(npix, dtype=np.uint32)
+        out = np.empty((spp, 4, npix))
+        for s in range(spp):
+            out[s, 0], out[s, 1] = self.pair(pix, sample_base + s, TAG_RAYGEN, 0)
+            out[s, 2], out[s, 3] = self.pair(pix, sample_base + s, TAG_RAYGEN, 1)
+        return out
+
+
+TAG_RAYGEN = 0xCA3E0000
+PRIMARY_PATH = 0x5EED0000  # k_primary / k_frame: path of sample s = mix32(PRIMARY_PATH, s)
+TRACE_PATH = 0x7A11  # srt_trace: path of batch ray i = mix32(TRACE_PATH, i)
+TAG_DIFFUSE, TAG_MC = 0xD1000000, 0x3C000000
+
+
+class Rays:
+    """A batch: origin/dir (3, n), medium index n (3, n) or (3, 1), batch-scalar counters.  With a
+    DeviceStream, `pix` (global pixel), `path` (child-path hash) and `rnd` (tie round of the hit
+    being shaded) identify each ray's random numbers as on the device; otherwise they are None."""
+
+    def __init__(self, O, D, n, depth, diffuse_reflections=0, pix=None, path=None):
         self.O, self.D, self.n = O, D, n
         self.depth = depth
         self.dfl = diffuse_reflections
+        self.pix, self.path, self.rnd = pix, path, None
 
     def __len__(self):
         return self.O.shape[1]
 
     def take(self, mask):
         n = self.n if self.n.shape[1] == 1 else self.n[:, mask]
-        return Rays(self.O[:, mask], self.D[:, mask], n, self.depth, self.dfl)
+        r = Rays(self.O[:, mask], self.D[:, mask], n, self.depth, self.dfl)
+        if self.path is not None:
+            r.pix, r.path = self.pix[mask], self.path[mask]
+            if self.rnd is not None:
+                r.rnd = self.rnd[mask]
+        return r
+
+    def child(self, O, D, n, depth, dfl, slot):
+        """A child batch of this (shaded) batch: RNG identity child_path(path, slot, round)."""
+        r = Rays(O, D, n, depth, dfl)
+        if self.path is not None:
+            r.pix, r.path = self.pix, child_path(self.path, slot, self.rnd)
+        return r
+
+
+_RNG = {"stream": None}  # DeviceStream while render_linear / trace run in device-stream mode
 
 
 def place(vals, mask):  # vec3.place (vector3.py:195-200)
@@ -251,7 +346,7 @@ def shade_glossy(scene, m, c, r, t, orient, counts):  # glossy.py:25-110
         F0 = col3(F0)
         cos_t = np.clip(dot(V, Nn), 0.0, 1.0)
         F = F0 + (1.0 - F0) * (1.0 - cos_t) ** 5
-        child = Rays(nudged, reflect(r.D, Nn), r.n, r.depth + 1, r.dfl)
+        child = r.child(nudged, reflect(r.D, Nn), r.n, r.depth + 1, r.dfl, 1)
         color = color + raycolor(scene, child, counts) * F
     return color
 
@@ -272,16 +367,20 @@ def shade_refractive(scene, m, c, r, t, orient, counts):  # refractive.py:24-123
     r_par = -1.0 * (n1 * cos_t - n2 * cos_i) / (n1 * cos_t + n2 * cos_i)
     F = (np.abs(r_per) ** 2 + np.abs(r_par) ** 2) / 2.0
     T = 1.0 - F
-    refl = Rays(nudged, reflect(r.D, Nn), n1, r.depth + 1, r.dfl)
+    refl = r.child(nudged, reflect(r.D, Nn), n1, r.depth + 1, r.dfl, 1)
     aver = (ratio[0] + ratio[1] + ratio[2]) / 3
     sin2 = aver ** 2 * (1.0 - cos_i ** 2)
     non_tir = sin2 <= 1.0
     Rt = normalize(r.D * aver + Nn * (aver * cos_i - np.sqrt(1 - np.clip(sin2, 0, 1))))
-    refr = Rays(P - Nn * 0.000001, Rt, n2, r.depth + 1, r.dfl)
+    refr = r.child(P - Nn * 0.000001, Rt, n2, r.depth + 1, r.dfl, 2)
     if c.assigned_primitive.mc:
-        pick = (np.random.rand(len(refl)) > (F[0] + F[1] + F[2]) / 3) & non_tir
-        both = Rays(np.where(pick, refr.O, refl.O), np.where(pick, refr.D, refl.D), np.where(pick, n2, n1),
-                    r.depth + 1, r.dfl)
+        if _RNG["stream"] is None:
+            u = np.random.rand(len(refl))  # refractive.py:100
+        else:
+            u = _RNG["stream"].pair(r.pix, r.path, TAG_MC | (r.depth << 8) | r.rnd, 0)[0]
+        pick = (u > (F[0] + F[1] + F[2]) / 3) & non_tir
+        both = r.child(np.where(pick, refr.O, refl.O), np.where(pick, refr.D, refl.D), np.where(pick, n2, n1),
+                       r.depth + 1, r.dfl, 1)
         color = raycolor(scene, both, counts)
     else:
         color = raycolor(scene, refl, counts) * F
@@ -306,9 +405,9 @@ def shade_thinfilm(scene, m, c, r, t, orient, counts):  # thin_film_interference
     else:
         Fim = lut[(cos_i * lut.shape[0]).astype(int), int(m.thickness)]
     F = np.array([Fim[:, 0], Fim[:, 1], Fim[:, 2]])
-    refl = Rays(P + Nn * 0.000001, reflect(r.D, Nn), r.n, r.depth + 1, r.dfl)
+    refl = r.child(P + Nn * 0.000001, reflect(r.D, Nn), r.n, r.depth + 1, r.dfl, 1)
     color = (col3(scene.ambient_color) + raycolor(scene, refl, counts)) * F
-    trans = Rays(P - Nn * 0.000001, r.D, r.n, r.depth + 1, r.dfl)
+    trans = r.child(P - Nn * 0.000001, r.D, r.n, r.depth + 1, r.dfl, 2)
     return color + raycolor(scene, trans, counts) * (1.0 - F)
 
 
@@ -332,17 +431,18 @@ def _onb(w):
     return cr(w, v), v
 
 
-def _cosine_generate(size, Nn):
+def _cosine_generate(size, Nn, draws=None):
     u, v = _onb(Nn)
-    phi = np.random.rand(size) * 2 * np.pi
-    r2 = np.random.rand(size)
+    a, r2 = (np.random.rand(size), np.random.rand(size)) if draws is None else draws
+    phi = a * 2 * np.pi
     z = np.sqrt(1 - r2)
     return u * (np.cos(phi) * np.sqrt(r2)) + v * (np.sin(phi) * np.sqrt(r2)) + Nn * z
 
 
-def _caps_generate(size, origin, prims):
+def _caps_generate(size, origin, prims, draws=None):
     nl = len(prims)
-    pick = (np.random.rand(size) * nl).astype(int)
+    pick_u = np.random.rand(size) if draws is None else draws[0]
+    pick = (pick_u * nl).astype(int)
     ws, cmaxs, us, vs = [], [], [], []
     for p in prims:
         tc = col3(p.center) - origin
@@ -352,8 +452,8 @@ def _caps_generate(size, origin, prims):
         ws.append(w), us.append(u), vs.append(v)
         cmaxs.append(np.sqrt(1 - np.clip(p.bounded_sphere_radius / dist, 0.0, 1.0) ** 2))
     masks = [pick == i for i in range(nl)]
-    phi = np.random.rand(size) * 2 * np.pi
-    r2 = np.random.rand(size)
+    a, r2 = (np.random.rand(size), np.random.rand(size)) if draws is None else draws[1:]
+    phi = a * 2 * np.pi
     cmax = np.select(masks, cmaxs)
     sel = lambda lst: np.array([np.select(masks, [x[k] for x in lst]) for k in range(3)])
     z = 1.0 + r2 * (cmax - 1.0)
@@ -379,18 +479,30 @@ def shade_diffuse(scene, m, c, r, t, orient, counts):  # diffuse.py:25-124
     Nr, Or = np.repeat(Nn, k, axis=1), np.repeat(nudged, k, axis=1)
     size = Nr.shape[1]
     prims = scene.importance_sampled_list
+    stream = _RNG["stream"]
+    cos_draws = caps_draws = sel = cpix = cpath = None
+    if r.path is not None:
+        # child j of ray i: child_path(path_i, 0x100 + j, round_i); Rng calls 0: (mixture select,
+        # unused), 1: cosine (phi, r2) or caps (pick, phi), 2: caps r2 (rt_device.h diffuse_child)
+        cpix = np.repeat(r.pix, k)
+        cpath = child_path(np.repeat(r.path, k), 0x100 + np.tile(np.arange(k), len(r)), np.repeat(r.rnd, k))
+    if stream is not None:
+        tag = TAG_DIFFUSE | r.depth
+        sel = stream.pair(cpix, cpath, tag, 0)[0]
+        cos_draws = caps_draws = stream.pair(cpix, cpath, tag, 1)
+        caps_draws = caps_draws + (stream.pair(cpix, cpath, tag, 2)[0],)
     if not prims:
-        d = _cosine_generate(size, Nr)
+        d = _cosine_generate(size, Nr, cos_draws)
         pdf = np.clip(dot(d, Nr), 0.0, 1.0) / np.pi
     else:
         w = m.ambient_weight
-        mask = np.random.rand(size)
-        d1 = _cosine_generate(size, Nr)
-        d2, ws, cm = _caps_generate(size, Or, prims)
+        mask = np.random.rand(size) if stream is None else sel
+        d1 = _cosine_generate(size, Nr, cos_draws)
+        d2, ws, cm = _caps_generate(size, Or, prims, caps_draws)
         d = np.where(mask < w, d1, d2)
         pdf = (np.clip(dot(d, Nr), 0.0, 1.0) / np.pi) * w + _caps_value(d, ws, cm) * (1.0 - w)
     nr = r.n if r.n.shape[1] == 1 else np.repeat(r.n, k, axis=1)
-    child = Rays(Or, d, nr, r.depth + 1, r.dfl + 1)
+    child = Rays(Or, d, nr, r.depth + 1, r.dfl + 1, cpix, cpath)
     ndl = np.clip(dot(d, Nr), 0.0, 1.0)
     if k == 1 and r.dfl >= 1:  # second bounce (diffuse.py:85-121)
         return diff * raycolor(scene, child, counts) * ndl / pdf / np.pi
@@ -430,11 +542,19 @@ def raycolor(scene, r, counts):
     counts["depth"][r.depth] = counts["depth"].get(r.depth, 0) + len(r)
     near, dists = nearest(scene, r.O, r.D)
     color = np.zeros((3, len(r)))
+    # tie round of each (ray, collider) hit: earlier colliders hit at the same distance (the device
+    # shades the first one in round 0 and the tied ones in rounds 1, 2, ...)
+    rnd = np.zeros(len(r), dtype=np.int64) if r.path is not None else None
     for c, d in zip(scene.collider_list, dists):
         hit = (near != FARAWAY) & (d[0] == near)
         if np.any(hit):
-            cc = shade(scene, c, r.take(hit), d[0][hit], d[1][hit], counts)
+            sub = r.take(hit)
+            if rnd is not None:
+                sub.rnd = rnd[hit]
+            cc = shade(scene, c, sub, d[0][hit], d[1][hit], counts)
             color = color + place(cc, hit)
+            if rnd is not None:
+                rnd = rnd + hit
     return color
 
 
@@ -469,18 +589,44 @@ def scene_medium(scene):
     return np.array([[scene.n.x], [scene.n.y], [scene.n.z]])
 
 
-def render_linear(scene, jitter):
+def render_linear(scene, jitter, stream=None, sample_base=0):
     """Sum over samples of raycolor / spp.  jitter (spp, 4, n).  Returns rgb (3, n), hit ids
-    (spp, n) of the primary rays, per-depth ray counts and the shadow-ray count."""
+    (spp, n) of the primary rays and the per-depth / shadow ray counts.  `stream`: a DeviceStream
+    for the Monte-Carlo draws (default: numpy's global RNG, the reference's order)."""
     spp = jitter.shape[0]
     counts = {}
     acc = 0.0
     ids = []
-    for s in range(spp):
-        O, D = primary_rays(scene.camera, jitter[s])
-        ids.append(hit_ids(scene, O, D)[1])
-        acc = acc + raycolor(scene, Rays(O, D, scene_medium(scene), 0, 0), counts)
+    _RNG["stream"] = stream
+    try:
+        for s in range(spp):
+            O, D = primary_rays(scene.camera, jitter[s])
+            ids.append(hit_ids(scene, O, D)[1])
+            r = Rays(O, D, scene_medium(scene), 0, 0)
+            if stream is not None:
+                n = D.shape[1]
+                r.pix = np.arange(n, dtype=np.uint32)
+                r.path = np.full(n, mix32(PRIMARY_PATH, sample_base + s), dtype=np.uint32)
+            acc = acc + raycolor(scene, r, counts)
+    finally:
+        _RNG["stream"] = None
     return acc / spp, np.array(ids), counts
+
+
+def trace_linear(scene, O, D, n, depth, dfl=0, stream=None):
+    """get_raycolor of one batch (srt_trace), MC draws from `stream` when given (ray i is keyed
+    like the device: pixel i, path mix32(TRACE_PATH, i))."""
+    r = Rays(O, D, n, depth, dfl)
+    counts = {}
+    _RNG["stream"] = stream
+    try:
+        if stream is not None:
+            k = D.shape[1]
+            r.pix = np.arange(k, dtype=np.uint32)
+            r.path = mix32(TRACE_PATH, np.arange(k, dtype=np.uint32))
+        return raycolor(scene, r, counts), counts
+    finally:
+        _RNG["stream"] = None
 
 
 def srgb_u8(rgb_lin, H, W):  # colour_functions.py:4-18 + scene.py:125-140

@@ -28,6 +28,16 @@ struct Scene {
 
 thread_local BvhBuild g_bvh;  // the BVH of the scene of the current call
 thread_local int g_use_bvh = 1;
+// rows of the current hc_render (null: identity / hc_trace): Monte-Carlo draws are keyed by the
+// global pixel, as key_pix in rt_kernels.hip
+thread_local const int32_t* g_rows = nullptr;
+thread_local int64_t g_width = 0;
+
+uint32_t key_pix(uint32_t pix) {
+    if (!g_rows) return pix;
+    const uint32_t W = (uint32_t)g_width, lr = pix / W;
+    return (uint32_t)g_rows[lr] * W + (pix - lr * W);
+}
 
 SceneView view_of(const srt_scene_desc* d) {
     SceneView S{};
@@ -92,7 +102,7 @@ struct HostEmit {
         for (int k = 0; k < g.count; ++k) {
             Rng rng;
             const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(seed, r.pix, cpath, 0xD1000000u | (uint32_t)depth);
+            rng.init(seed, key_pix(r.pix), cpath, 0xD1000000u | (uint32_t)depth);
             push(diffuse_child(S, S.mat[mi], g, rng, (uint32_t)k), cpath);
         }
     }
@@ -101,7 +111,7 @@ struct HostEmit {
 double mc_uniform(const SceneView& S, uint64_t seed, int depth, const Ray& r, int cid, uint32_t round) {
     if (!(S.col[cid].flags & SRT_CF_MC)) return 0.0;
     Rng g;
-    g.init(seed, r.pix, r.path, 0x3C000000u | ((uint32_t)depth << 8) | round);
+    g.init(seed, key_pix(r.pix), r.path, 0x3C000000u | ((uint32_t)depth << 8) | round);
     return g.one();
 }
 
@@ -157,6 +167,8 @@ int hc_render(const srt_scene_desc* d, const srt_camera* cam, const srt_render_a
     int64_t shadow = 0;
     srt_stats stats{};
     const int dcap = depth_cap(d);
+    g_rows = a->rows;
+    g_width = W;
     for (int s = 0; s < a->spp; ++s) {
         std::vector<Ray> cur, next;
         for (int64_t p = 0; p < npix; ++p) {
@@ -209,6 +221,7 @@ int hc_render(const srt_scene_desc* d, const srt_camera* cam, const srt_render_a
 
 int hc_trace(const srt_scene_desc* d, const srt_trace_args* a, srt_stats* st) {
     SceneView S = view_of(d);
+    g_rows = nullptr;
     const int64_t n = a->n;
     std::vector<double> fb(3 * n, 0.0);
     std::vector<Ray> cur, next;
@@ -235,6 +248,7 @@ int hc_trace(const srt_scene_desc* d, const srt_trace_args* a, srt_stats* st) {
     if (!cur.empty()) { g_err = "rays alive after the depth cap"; return SRT_ERR_DEPTH; }
     if (int rc = err_code(err)) return rc;
     std::memcpy(a->out_rgb, fb.data(), 3 * n * sizeof(double));
+    stats.n_depths = dlast + 1;
     for (int k = 0; k < SRT_MAX_DEPTHS; ++k) stats.total_rays += stats.rays_per_depth[k];
     stats.shadow_rays = shadow;
     if (st) *st = stats;
@@ -276,6 +290,13 @@ int hc_primary_rays(const srt_camera* cam, const double* J, double* O, double* D
     }
     return SRT_OK;
 }
+
+// rt_device.h's Philox4x32-10 and path hash (known-answer tests of the Monte-Carlo stream)
+void hc_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out) {
+    const u4 r = philox(u4{ctr[0], ctr[1], ctr[2], ctr[3]}, k0, k1);
+    out[0] = r.a; out[1] = r.b; out[2] = r.c; out[3] = r.d;
+}
+uint32_t hc_mix32(uint32_t h, uint32_t v) { return mix32(h, v); }
 
 // numpy legacy rand stream by the segmented jump-ahead scheme of rt_mt.h, run serially
 int hc_mt_uniforms(const uint32_t* key, int pos, int64_t n_out, int64_t n_skip, double* out, uint32_t* key_out,

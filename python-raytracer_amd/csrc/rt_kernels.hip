@@ -58,6 +58,10 @@ constexpr int BLOCK = 256;
 constexpr int NSHARD = RT_NSHARD;
 constexpr size_t TRACE_PARAMS_BYTES = 784;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
+// retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
+// a chained ray a second child (re-render without chain mode)
+constexpr uint32_t RETRY_OVERFLOW = 1u;
+constexpr uint32_t RETRY_CHAIN_TIE = 2u;
 
 struct Queue {
     double *ox, *oy, *oz, *dx, *dy, *dz, *wr, *wg, *wb;
@@ -103,6 +107,16 @@ struct TraceParams {
 // kernel argument: host and device passes must agree on the layout (catches address-space pointer
 // size differences, see SceneView)
 static_assert(sizeof(TraceParams) == TRACE_PARAMS_BYTES, "TraceParams layout");
+
+// Pixel identity that keys the Monte-Carlo draws: the global pixel row * width + col of the frame
+// (`pix` indexes the rows this call renders), so that an image sharded over any number of GPUs draws
+// the same numbers as the single-GPU render; srt_trace (no rows) keys by the ray's batch index.
+__device__ __forceinline__ uint32_t key_pix(const TraceParams& P, uint32_t pix) {
+    if (!P.rows) return pix;
+    const uint32_t W = (uint32_t)P.cam.width;
+    const uint32_t lr = pix / W;
+    return (uint32_t)P.rows[lr] * W + (pix - lr * W);
+}
 
 __device__ __forceinline__ void queue_store(const Queue& q, int64_t i, d3 o, d3 d, d3 w, uint32_t pix,
                                             uint32_t meta, uint32_t path) {
@@ -187,7 +201,7 @@ struct GpuEmit {
             queue_store(P.qout, (int64_t)shard * P.seg + slot, c.o, c.d, mul(r.w, c.w), r.pix,
                         pack_meta(c.medium, meta_depth(r.meta) + 1, c.dfl), path);
         } else {
-            P.flags[1] = 1u;
+            atomicOr(&P.flags[1], RETRY_OVERFLOW);
         }
     }
     __device__ void child(const Child& c) const {
@@ -200,7 +214,7 @@ struct GpuEmit {
         for (int k = 0; k < g.count; ++k) {
             Rng rng;
             const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(P.seed, r.pix, cpath, 0xD1000000u | meta_depth(r.meta));
+            rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
             store(slot + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
         }
     }
@@ -209,7 +223,7 @@ struct GpuEmit {
 __device__ __forceinline__ double mc_uniform(const TraceParams& P, const Ray& r, int cid, uint32_t round) {
     if (!(P.S.col[cid].flags & SRT_CF_MC)) return 0.0;
     Rng g;
-    g.init(P.seed, r.pix, r.path, 0x3C000000u | (meta_depth(r.meta) << 8) | round);
+    g.init(P.seed, key_pix(P, r.pix), r.path, 0x3C000000u | (meta_depth(r.meta) << 8) | round);
     return g.one();
 }
 
@@ -395,7 +409,7 @@ struct ChainEmit {
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void put(const Child& c, uint32_t path) const {
         if (*has) {
-            P.flags[1] = 2u;
+            atomicOr(&P.flags[1], RETRY_CHAIN_TIE);
             return;
         }
         *has = true;
@@ -412,7 +426,7 @@ struct ChainEmit {
         for (int k = 0; k < g.count; ++k) {
             Rng rng;
             const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(P.seed, r.pix, cpath, 0xD1000000u | meta_depth(r.meta));
+            rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
             put(diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
         }
     }
@@ -552,7 +566,7 @@ struct FrameEmit {
         for (int k = 0; k < g.count; ++k) {
             Rng rng;
             const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(P.seed, r.pix, cpath, 0xD1000000u | meta_depth(r.meta));
+            rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
             store(pos + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
         }
     }
@@ -671,7 +685,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     for (int d = lane; d <= P.dcap + 1 && d < SRT_MAX_DEPTHS; d += FRAME_BLOCK)
         if (L.depth_cnt[d]) atomicAdd(P.cnt_out + (int64_t)d * NSHARD + shard, L.depth_cnt[d]);
     if (err) atomicOr(&P.flags[0], err);
-    if (lane == 0 && lds_get(&L.overflow)) atomicOr(&P.flags[1], 1u);
+    if (lane == 0 && lds_get(&L.overflow)) atomicOr(&P.flags[1], RETRY_OVERFLOW);
     // the wave's shadow-ray count into its shard's counter
     for (int off = 32; off > 0; off >>= 1) shadow += __shfl_xor(shadow, off);
     if (lane == 0) {
@@ -1269,17 +1283,19 @@ namespace {
 // Read back a completed frame (its stream has been synchronised): error/overflow flags OR-ed over
 // every pass (and every asynchronous frame since the last synchronisation point), per-depth counts
 // and kernel times of the frame's passes.  Returns SRT_RETRY_OVERFLOW when a queue shard overflowed.
-constexpr int SRT_RETRY_OVERFLOW = 1;
-int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S) {
-    bool overflow = false;
+// `retry` receives the RETRY_* bits of every pass.
+constexpr int SRT_RETRY = 1;
+int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S, uint32_t* retry = nullptr) {
+    uint32_t bits = 0;
     for (int p = 0; p < F.npass; ++p) {
         const uint32_t* hp = c->f->host + p * F.pass_words;
         int rc;
         if ((rc = check_flags(hp[F.cnt_words]))) return rc;
-        overflow |= hp[F.cnt_words + 1] != 0;
-        if (hp[F.cnt_words + 1] & 2u) c->chain_ok = false;  // a tie gave a chained ray two children
+        bits |= hp[F.cnt_words + 1];
     }
-    if (overflow) return SRT_RETRY_OVERFLOW;
+    if (bits & RETRY_CHAIN_TIE) c->chain_ok = false;  // no chain mode for this scene any more
+    if (retry) *retry = bits;
+    if (bits) return SRT_RETRY;
     double ms_trace = 0.0, ms_primary = 0.0;
     for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.rays_per_depth[d] = 0;
     for (int p = 0; p < F.npass; ++p) {
@@ -1371,12 +1387,14 @@ int finish_async(srt_ctx* c, srt_stats* st) {
         if (!f.pending) continue;
         c->f = &f;
         srt_stats S{};
-        int rc = collect_frame(c, f.plan, S);
+        uint32_t bits = 0;
+        int rc = collect_frame(c, f.plan, S, &bits);
         clear_host_flags(c, f.plan);
         f.pending = 0;
-        if (rc == SRT_RETRY_OVERFLOW) {
+        if (rc == SRT_RETRY) {
             overflow = true;
-            if ((rc = f.plan.frame ? ensure_ring(c, 2 * f.ring_cap) : ensure_queues(c, 2 * f.seg * NSHARD))) {
+            if ((bits & RETRY_OVERFLOW) &&
+                (rc = f.plan.frame ? ensure_ring(c, 2 * f.ring_cap) : ensure_queues(c, 2 * f.seg * NSHARD))) {
                 first_err = first_err ? first_err : rc;
             }
         } else if (rc) {
@@ -1388,8 +1406,8 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     c->f = &c->slots[0];
     if (first_err) return first_err;
     if (overflow)
-        return fail(SRT_ERR_MEMORY, "a ray queue overflowed during an asynchronous frame (queues grown; render "
-                                    "that frame again)");
+        return fail(SRT_ERR_MEMORY, "a ray queue overflowed (queues grown) or a tie met chain mode (chain mode "
+                                    "off) during an asynchronous frame: render that frame again");
     c->async_stats = last;
     if (st) *st = last;
     return SRT_OK;
@@ -1851,12 +1869,17 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         HIP_TRY(hipStreamSynchronize(c->f->stream));
         c->f->dirty = false;
         const int64_t retries = S.retries;
-        rc = collect_frame(c, F, S);
-        if (rc == SRT_RETRY_OVERFLOW) {
-            // a queue shard overflowed: grow the queues and render the frame again
+        uint32_t bits = 0;
+        rc = collect_frame(c, F, S, &bits);
+        if (rc == SRT_RETRY) {
+            // render the frame again: without chain mode after a tie gave a chained ray a second
+            // child (the same tie would recur), with bigger queues after an overflow
             S.retries = retries + 1;
             if (S.retries > 8) return fail(SRT_ERR_MEMORY, "ray queues keep overflowing");
-            if ((rc = F.frame ? ensure_ring(c, 2 * c->f->ring_cap) : ensure_queues(c, 2 * c->f->seg * NSHARD))) return rc;
+            if (bits & RETRY_CHAIN_TIE) F.chain_from = 0;
+            if ((bits & RETRY_OVERFLOW) &&
+                (rc = F.frame ? ensure_ring(c, 2 * c->f->ring_cap) : ensure_queues(c, 2 * c->f->seg * NSHARD)))
+                return rc;
             continue;
         }
         S.retries = retries;

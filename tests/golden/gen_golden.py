@@ -173,6 +173,50 @@ def gen_features(sp):
         print(name, "rays per depth", counts.tolist(), "rgb mean", lin.mean())
 
 
+MC_CONFIGS = [
+    # name, W, H, depth, spp, seed: Monte-Carlo refraction (Primitive.mc, refractive.py:95-101) -- the
+    # glass sphere of the cornell box / of tests/scenes.py:features with mc=True, rendered by the
+    # reference in one process (seeded, hence deterministic)
+    ("cornell_mc_24x24_s1", 24, 24, None, 1, 0),
+    ("features_mc_48x36_d4_s2", 48, 36, 4, 2, 0),
+]
+
+
+def gen_mc(sp):
+    sys.path.insert(0, str(OUT.parent))
+    import scenes
+
+    for name, W, H, depth, spp, seed in MC_CONFIGS:
+        if name.startswith("cornell"):
+            scene = capture_scene(sp, "example_cornellbox.py", W, H, depth)
+            glass = [p for p in scene.scene_primitives if type(p.material).__name__ == "Refractive"]
+            assert len(glass) == 1
+            glass[0].mc = True
+        else:
+            scene = scenes.features(W, H, depth, sp=sp, mc=True)
+        lin, u8, hits, nears, counts = render_golden(sp, scene, spp, seed)
+        np.savez_compressed(OUT / (name + ".npz"), rgb=lin, srgb8=u8, hit_id=hits.astype(np.int16), nearest=nears,
+                            depth_counts=counts, seed=seed, spp=spp, width=W, height=H, depth=-1 if depth is None else depth)
+        print(name, "rays per depth", counts.tolist(), "rgb mean", lin.mean())
+
+
+# SURVEY 8(c) statistical pin of the cornell box: per-seed means of every 10x10 pixel block (linear
+# RGB) of single-process seeded renders by the reference
+CORNELL_STATS = ("cornell_stats_80x80", 80, 80, 8, 16)  # name, W, H, spp per seed, seeds
+
+
+def gen_cornell_stats(sp):
+    name, W, H, spp, nseeds = CORNELL_STATS
+    scene = capture_scene(sp, "example_cornellbox.py", W, H, None)
+    blocks = np.empty((nseeds, 3, H // 10, W // 10))
+    for s in range(nseeds):
+        lin, _, _, _, counts = render_golden(sp, scene, spp, 1000 + s)
+        blocks[s] = lin.reshape(3, H // 10, 10, W // 10, 10).mean(axis=(2, 4))
+        print(name, "seed", s, "rays", int(counts.sum()), "mean", lin.mean())
+    np.savez_compressed(OUT / (name + ".npz"), block_means=blocks, seeds=1000 + np.arange(nseeds), spp=spp, width=W,
+                        height=H, block=10)
+
+
 def gen_colliders(sp):
     """Known-answer tests of every collider's intersect on random and edge-case rays."""
     from sightpy.geometry.triangle import Triangle_Collider
@@ -258,6 +302,10 @@ if __name__ == "__main__":
         gen_textures(sp)
     if not only or "features" in only:
         gen_features(sp)
-    rest = [o for o in only if o not in ("colliders", "camera", "textures", "features")]
+    if not only or "mc" in only:
+        gen_mc(sp)
+    if not only or "cornell_stats" in only:
+        gen_cornell_stats(sp)
+    rest = [o for o in only if o not in ("colliders", "camera", "textures", "features", "mc", "cornell_stats")]
     if not only or rest:
         gen_examples(sp, rest or None)

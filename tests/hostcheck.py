@@ -32,6 +32,9 @@ def lib():
         _lib.hc_mt_uniforms.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         _lib.hc_last_error.restype = ctypes.c_char_p
+        _lib.hc_philox.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        _lib.hc_mix32.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        _lib.hc_mix32.restype = ctypes.c_uint32
         _lib.hc_set_bvh.argtypes = [ctypes.c_int]
         _lib.hc_bvh_nodes.argtypes = [ctypes.POINTER(N.SceneDesc)]
     return _lib
@@ -106,3 +109,36 @@ def mt_uniforms(key, pos, n_out, n_skip=0):
                               key_out.ctypes.data, ctypes.byref(pos_out))
     assert rc == 0, rc
     return out, key_out, pos_out.value
+
+
+def philox(ctr, k0, k1):
+    """rt_device.h philox(ctr[4], k0, k1) -> 4 uint32."""
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    out = np.empty(4, dtype=np.uint32)
+    lib().hc_philox(c.ctypes.data, int(k0), int(k1), out.ctypes.data)
+    return out
+
+
+def mix32(h, v):
+    return int(lib().hc_mix32(int(h), int(v)))
+
+
+def trace(scene, O, D, depth=0, dfl=0, seed=0, medium=None):
+    """hc_trace: get_raycolor of a batch (3, n) on the CPU build of the kernels."""
+    L = lower_scene(scene)
+    d = L.desc()
+    O = np.ascontiguousarray(O, dtype=np.float64)
+    D = np.ascontiguousarray(D, dtype=np.float64)
+    n = O.shape[1]
+    a = N.TraceArgs()
+    a.n, a.origin, a.dir = n, N.ptr(O), N.ptr(D)
+    med = None if medium is None else np.ascontiguousarray(medium, dtype=np.int32)
+    a.medium = N.ptr(med)
+    a.depth, a.diffuse_reflections, a.seed = depth, dfl, seed
+    out = np.empty((3, n))
+    a.out_rgb = N.ptr(out)
+    st = N.Stats()
+    rc = lib().hc_trace(ctypes.byref(d), ctypes.byref(a), ctypes.byref(st))
+    if rc:
+        raise RuntimeError(lib().hc_last_error().decode())
+    return out, st.as_dict()

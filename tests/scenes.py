@@ -87,7 +87,9 @@ def example4(width=400, height=300, depth=None):
     return _depth(sc, depth)
 
 
-def cornell(width=100, height=100, depth=None):
+def cornell(width=100, height=100, depth=None, mc=False):
+    """example_cornellbox.py; `mc=True` makes the glass sphere pick reflection or refraction by
+    Monte Carlo (refractive.py:95-101), which no example script does."""
     sc = Scene(ambient_color=rgb(0.00, 0.00, 0.00))
     sc.add_Camera(screen_width=width, screen_height=height, look_from=vec3(278, 278, 800),
                   look_at=vec3(278, 278, 0), focal_distance=1.0, field_of_view=40)
@@ -113,7 +115,7 @@ def cornell(width=100, height=100, depth=None):
     cb.rotate(θ=15, u=vec3(0, 1, 0))
     sc.add(cb)
     sc.add(Sphere(material=glass, center=vec3(370.5, 165 / 2, -65 - 185 / 2), radius=165 / 2, shadow=False,
-                  max_ray_depth=3), importance_sampled=True)
+                  max_ray_depth=3, mc=mc), importance_sampled=True)
     return _depth(sc, depth)
 
 
@@ -121,14 +123,15 @@ BUILDERS = {"example1": example1, "example2": example2, "example3": example3, "e
             "cornell": cornell}
 
 
-def features(width=64, height=48, depth=4, sp=None):
+def features(width=64, height=48, depth=4, sp=None, mc=False):
     """Feature scene (not one of the reference's scripts): exercises the API paths the examples do
     not reach -- normal map on a textured floor (material.py:18-40), a rotated textured Cuboid
     (cuboid.py:84-187 uv cross), an absorbing glass sphere, an Emissive sphere, a metal with
     roughness, two directional lights and a spherical Panorama background (panorama.py:10-26).
 
     `sp` is the sightpy module to build with: this package by default; tests/golden/gen_golden.py
-    passes the reference's module so the fixture comes from the reference itself."""
+    passes the reference's module so the fixture comes from the reference itself.  `mc=True`: the
+    glass sphere picks reflection or refraction by Monte Carlo (refractive.py:95-101)."""
     if sp is None:
         import sightpy as sp
     vec3, rgb = sp.vec3, sp.rgb
@@ -152,7 +155,8 @@ def features(width=64, height=48, depth=4, sp=None):
                    max_ray_depth=depth, shadow=True)
     cb.rotate(θ=25, u=vec3(0, 1, 0))
     sc.add(cb)
-    sc.add(sp.Sphere(material=glass, center=vec3(0.6, 0.0, -0.8), radius=0.5, max_ray_depth=depth, shadow=False))
+    sc.add(sp.Sphere(material=glass, center=vec3(0.6, 0.0, -0.8), radius=0.5, max_ray_depth=depth, shadow=False,
+                     mc=mc))
     sc.add(sp.Sphere(material=metal, center=vec3(0.1, -0.25, 0.2), radius=0.25, max_ray_depth=depth))
     sc.add(sp.Sphere(material=lamp, center=vec3(1.5, 0.8, -2.0), radius=0.3, max_ray_depth=depth, shadow=False))
     sc.add_Background("miramar.jpeg", spherical=True)

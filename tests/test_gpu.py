@@ -176,6 +176,22 @@ def test_example1_1080p_d5_properties():
                                atol=1e-14)
 
 
+@pytest.mark.parametrize("builder,depth,spp,seed", [(scenes.example1, 5, 2, 0), (scenes.example3, 8, 1, 0)],
+                         ids=["example1_1080p_d5_2spp", "example3_1080p_d8_1spp"])
+def test_headline_configs_1080p_rgb_match_oracle(builder, depth, spp, seed):
+    """Full-size RGB parity at the BASELINE headline configurations (1920x1080): hit ids exact,
+    per-depth ray counts equal, linear RGB within 1e-5 relative of the oracle on the same jitter."""
+    sc = builder(1920, 1080, depth)
+    np.random.seed(seed)
+    jit = sc.camera.draw_jitter(spp)
+    out = _backend().render_scene(sc, spp, jitter=jit, seed=1, want_hits=True)
+    rgb, ids, counts = O.render_linear(sc, jit)
+    assert np.array_equal(out.hit_ids, ids)
+    assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+    np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
+    _close_u8(out.srgb8, O.srgb_u8(rgb, 1080, 1920))
+
+
 def test_example1_1080p_d5_ray_counts_match_reference_survey():
     # SURVEY.md section 6: seed 0, 6 spp -> rays per depth measured with the reference
     sc = scenes.example1(1920, 1080, 5)
@@ -367,3 +383,28 @@ def test_gpu_degenerate_scenes(which):
     np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
     if which == "no_background":
         assert (ids == -1).any()
+
+
+def test_gpu_chain_mode_recovers_from_ties(tmp_path):
+    """A tie (duplicated mesh faces: two colliders at the same distance, both shaded, ray.py:131-146)
+    gives a chained ray two children.  The frame is rendered again without chain mode (not with
+    bigger queues, which would never help), and the result equals the oracle."""
+    path = str(tmp_path / "ico_dup.obj")
+    scenes.write_icosphere_obj(path, subdiv=2, duplicate_faces=320)  # every face twice
+    sc = scenes.mesh_scene(path, 48, 36, 3)
+    np.random.seed(9)
+    jit = sc.camera.draw_jitter(2)
+    _set_option("frame_kernel", 0)
+    _set_option("chain_rays", 1 << 40)
+    try:
+        B = _backend()
+        outs = [B.render_scene(sc, 2, jitter=jit, seed=1, want_hits=True) for _ in range(3)]
+    finally:
+        _set_option("frame_kernel", -1)
+        _set_option("chain_rays", 1000000)
+    rgb, ids, counts = O.render_linear(sc, jit)
+    for out in outs:
+        assert np.array_equal(out.hit_ids, ids)
+        assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+        np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
+    assert all(out.stats["retries"] <= 1 for out in outs)
