@@ -127,16 +127,15 @@ def test_get_distances_matches_oracle():
     assert np.array_equal(img[..., 0], ref)
 
 
-def test_cornell_monte_carlo_statistics():
+def test_cornell_monte_carlo_deterministic():
+    """(Sample-for-sample parity of the MC paths: tests/test_gpu_mc.py.)  The primary hit ids match
+    the reference's fixture, and the device RNG is deterministic: identical seeds, identical images."""
     g = golden("cornell_24x24_s1")
     sc = scenes.cornell(24, 24)
     np.random.seed(0)
     jit = sc.camera.draw_jitter(16)
     out = _backend().render_scene(sc, 16, jitter=jit, seed=3, want_hits=True)
     assert np.array_equal(out.hit_ids[0], g["hit_id"][0])
-    ref, got = g["rgb"].mean(), out.rgb.mean()
-    assert abs(got - ref) / ref < 0.1, (got, ref)
-    # deterministic device RNG: identical seeds give identical images
     out2 = _backend().render_scene(sc, 16, jitter=jit, seed=3)
     np.testing.assert_allclose(out2.rgb, out.rgb, rtol=1e-12, atol=1e-12)
 

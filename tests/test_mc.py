@@ -102,7 +102,10 @@ def test_device_math_diffuse_batch_kat(dfl):
     sc = scenes.cornell(16, 16)
     rng = np.random.default_rng(dfl)
     n = 300
-    Ob = np.array([[278.0], [278.0], [-278.0]]) + rng.uniform(-150, 150, (3, n))
+    # origins in the box above the tall block and the glass sphere (a ray starting inside the block
+    # meets its bottom face and the coplanar floor at distances one rounding apart: a tie or not
+    # depending on the last bit of the direction, i.e. on the libm)
+    Ob = np.stack([rng.uniform(20, 535, n), rng.uniform(350, 540, n), rng.uniform(-535, -20, n)])
     D = rng.standard_normal((3, n))
     D /= np.sqrt((D * D).sum(0))
     got, st = HC.trace(sc, Ob, D, depth=0, dfl=dfl, seed=99)
