@@ -1,22 +1,32 @@
-"""Headline benchmark: Mrays/s (primary + secondary) on example1 at 1920x1080, depth 5, 6 spp
-(BASELINE.json configs[1]) through the C ABI of libsightpy_hip.so.
+"""Headline benchmark: Mrays/s (primary + secondary) and frame ms on example1 at 1920x1080, depth 5,
+6 spp (BASELINE.json configs[1]) through the C ABI of libsightpy_hip.so.
 
-One step = one full frame: every spp sample traced through every depth, plus the sRGB resolve, with
-the scene, camera tables and the sample jitter already resident in HBM (the jitter is the
-reference's numpy stream for seed 0, uploaded once before timing).  With N GPUs
-(torch.distributed, one process per GPU) the frame's rows are dealt round-robin in 8-row bands,
-each rank renders its shard and the uint8 tiles are gathered to rank 0 over RCCL; the frame is
-fixed, so scaling is strong.
+One step = one SURVEY 8(d) frame, from render() entry (scene already uploaded) to the image in host
+memory:
+  * the camera jitter is the reference's numpy stream (np.random.seed(0) before the first frame,
+    every frame continuing it, as consecutive Scene.render calls do), generated on the GPU inside the
+    step (rt_mt.h; bit-equal to np.random.rand);
+  * every sample traced through every depth, the sRGB resolve;
+  * the uint8 image and the linear RGB (f64) copied to pinned host memory.
+Frames are pipelined (each step queues its frame and returns; the timed region ends when all K
+frames are in host memory).  With N GPUs (one process per GPU, `torch.distributed.run` launches
+them; no torch is imported) the library splits each frame into 8-row bands dealt round-robin
+(SRT_RENDER_SHARDED), every rank draws the same stream and reads its rows, and the uint8 and
+linear-RGB tiles are gathered to rank 0 over RCCL (xGMI); the frame is fixed, so scaling is strong.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config example1_1080p_d5]
+Secondary figures in the same line: `frame_latency_ms` (one synchronous frame), `device_resident`
+(jitter pre-resident in HBM and outputs left in HBM: the round-1 headline), the roofline of the
+dominant kernel, and the CPU baseline (oracle: one core, and a multiprocessing.Pool over samples
+structured like the reference's Scene.render).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config example1_1080p_d5] [--rng mt|device]
 """
 import os
 
-os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # the CPU baseline is a single-core number
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # CPU baseline legs: one BLAS thread per process
 import argparse
 import ctypes
 import json
-import os
 import subprocess
 import sys
 import time
@@ -28,8 +38,8 @@ ROOT = Path(__file__).resolve().parent
 for p in (ROOT / "python-raytracer_amd", ROOT / "tests", ROOT / "oracle"):
     sys.path.insert(0, str(p))
 
-BYTES_PER_RAY = 280  # algorithmic bytes per ray segment of the fp64 wavefront
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFS = 78.6  # MI355X fp64 vector spec: 256 CU x 64 FMA/clk x 2 x 2.4 GHz
 
 CONFIGS = {
     # name: (builder, width, height, depth, spp, label)
@@ -42,13 +52,71 @@ CONFIGS = {
                       "TriangleMesh (20480-triangle icosphere, BVH) + sphere + floor + sky 1920x1080 depth 3, 2 spp"),
 }
 
+RAY_BYTES = 84  # one queued ray record (rt_kernels.hip Queue): O, D, throughput f64 x 9 + 3 u32
 
-def cpu_baseline(builder, W, H, depth, spp, budget_s=20.0):
-    """Oracle (numpy port of the reference algorithm) timed on this host's CPU, one process, on the
-    same frame: samples are traced one after another until the frame is done or `budget_s` of CPU
-    time is spent (the sample count is reported)."""
-    import sightpy_oracle as O
+
+def kernel_bytes_model(stats, spp, npix, lens):
+    """Algorithmic HBM bytes of one launch of the dominant kernel, from what it moves (DESIGN.md §3);
+    texture and scene-table reads are cache-resident and not counted.
+      k_primary (wavefront path): depth-0 rays are generated and shaded in registers, so jitter read
+        (2 f64 per sample, 4 for a thin lens) + the depth-1 children written to the queue (84 B) +
+        the framebuffer store (3 f64 per pixel);
+      k_frame (branching scenes, one pass): jitter read + every secondary ray written to and read
+        back from its wave's ring (2 x 84 B) + the fused resolve's uint8 and linear-RGB stores."""
+    planes = 4 if lens else 2
+    rpd = stats["rays_per_depth"]
+    if stats["kernel_path"] == "frame":
+        return spp * npix * planes * 8 + sum(rpd[1:]) * 2 * RAY_BYTES + npix * 27
+    children = rpd[1] if len(rpd) > 1 else 0
+    return spp * npix * planes * 8 + children * RAY_BYTES + npix * 24
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        for line in out.splitlines():
+            if "Model name" in line:
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def _pool_warm(args):
+    builder, W, H, depth = args
     import scenes
+    import sightpy_oracle  # noqa: F401
+
+    getattr(scenes, builder)(W, H, depth)
+    return os.getpid()
+
+
+def _pool_task(args):
+    """One Pool task: the oracle's get_raycolor of a batch of samples (reference scene.py:16-17,
+    98-116: each task traces its samples and returns their summed colour)."""
+    builder, W, H, depth, jit = args
+    import scenes
+    import sightpy_oracle as O
+
+    sc = getattr(scenes, builder)(W, H, depth)
+    counts = {}
+    acc = 0.0
+    for j in jit:
+        Oo, Do = O.primary_rays(sc.camera, j)
+        acc = acc + O.raycolor(sc, O.Rays(np.ascontiguousarray(np.broadcast_to(Oo, Do.shape)), Do,
+                                          O.scene_medium(sc), 0), counts)
+    return acc, sum(counts["depth"].values())
+
+
+def cpu_baseline(builder, W, H, depth, spp, budget_s=15.0):
+    """The oracle (numpy restatement of the reference, oracle/sightpy_oracle.py) timed on this host's
+    CPU on the same frame: (1) one core, samples one after another until the frame is done or
+    `budget_s` is spent; (2) a multiprocessing.Pool over samples structured like the reference's
+    Scene.render (scene.py:80-116: ceil(spp / workers) samples per task, results summed), with as
+    many workers as this process may use (capped at 16, the GPU box's CPU share per GPU)."""
+    import multiprocessing as mp
+    import scenes
+    import sightpy_oracle as O
 
     sc = getattr(scenes, builder)(W, H, depth)
     np.random.seed(0)
@@ -63,37 +131,69 @@ def cpu_baseline(builder, W, H, depth, spp, budget_s=20.0):
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    rays = sum(counts["depth"].values())
-    return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": "oracle/sightpy_oracle.py (numpy restatement of the reference), 1 process, "
-                      "OPENBLAS_NUM_THREADS=1: %d of %d samples of the same %dx%d frame (%d rays, %.1f s)"
-                      % (done, spp, W, H, rays, dt),
-            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count()}
+    rays1 = sum(counts["depth"].values())
+    one = {"value": round(rays1 / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
+           "sample": "oracle/sightpy_oracle.py, 1 process, OPENBLAS_NUM_THREADS=1: %d of %d samples of the same "
+                     "%dx%d frame (%d rays, %.1f s)" % (done, spp, W, H, rays1, dt)}
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    workers = max(1, min(avail, 16))
+    per_task = -(-spp // workers)
+    tasks = [(builder, W, H, depth, jit[i:i + per_task]) for i in range(0, spp, per_task)]
+    # spawned workers (fresh interpreters: this process holds the GPU, forked children would inherit
+    # its device handles), warmed up with the imports and scene build before the timed tasks
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(min(workers, len(tasks))) as pool:
+        pool.map(_pool_warm, [(builder, 8, 8, depth)] * min(workers, len(tasks)))
+        t0 = time.perf_counter()
+        res = list(pool.imap_unordered(_pool_task, tasks))
+        dtp = time.perf_counter() - t0
+    raysp = sum(r[1] for r in res)
+    pool_leg = {"value": round(raysp / dtp / 1e6, 4), "unit": "Mrays/s", "cores": min(workers, len(tasks)),
+                "workers": workers, "kind": "port",
+                "sample": "oracle/sightpy_oracle.py in multiprocessing.Pool(%d) over samples like scene.py:80-116 "
+                          "(%d tasks of %d sample(s)): the whole %dx%d %d-spp frame (%d rays, %.2f s wall incl. "
+                          "the scene build per task)" % (workers, len(tasks), per_task, W, H, spp, raysp, dtp)}
+    one.update({"cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "usable_cpus": avail, "pool": pool_leg})
+    return one
 
 
-def pmc_traffic(config, kernel="k_primary"):
-    """HBM bytes per k_primary launch from the newest committed PMC summary of this config
-    (profiles/rNN_traffic_<config>.json, written by tools/pmc_traffic.py from two separate
-    rocprofv3 --pmc passes of this same bench command), or None."""
+def pmc_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this config
+    (profiles/rNN_traffic_<config>.json, tools/pmc_traffic.py: separate rocprofv3 --pmc passes of
+    FETCH_SIZE (x2 on gfx950) and WRITE_SIZE of this bench), or None."""
     files = sorted(ROOT.glob("profiles/r*_traffic_%s.json" % config))
     if not files:
-        return None, None
+        return None, None, None
     rec = json.loads(files[-1].read_text())
     for name, k in rec["kernels"].items():
         if kernel in name and "traffic_bytes" in k:
-            return k["traffic_bytes"] / 1e9, files[-1].name
-    return None, None
+            return k["traffic_bytes"] / 1e9, files[-1].name, k
+    return None, None, None
 
 
-def _cpu_model():
-    try:
-        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
-        for line in out.splitlines():
-            if "Model name" in line:
-                return line.split(":", 1)[1].strip()
-    except Exception:
-        pass
-    return "unknown"
+def comm_id_exchange(lib, N, rank, world):
+    """RCCL unique id from rank 0 to every rank through a file keyed by the launcher's pid and port
+    (one node: torch.distributed.run starts every rank as a child of one agent process)."""
+    path = Path("/tmp") / ("sightpy_comm_%d_%s.id" % (os.getppid(), os.environ.get("MASTER_PORT", "0")))
+    buf = (ctypes.c_uint8 * N.COMM_ID_BYTES)()
+    if rank == 0:
+        N.check(lib, lib.srt_comm_unique_id(buf))
+        tmp = path.with_suffix(".tmp")
+        tmp.write_bytes(bytes(buf))
+        os.replace(tmp, path)
+    else:
+        t0 = time.time()
+        while not path.exists():
+            if time.time() - t0 > 120:
+                raise SystemExit("rank %d: no communicator id from rank 0 (%s)" % (rank, path))
+            time.sleep(0.02)
+        time.sleep(0.05)
+        data = path.read_bytes()
+        ctypes.memmove(buf, data, N.COMM_ID_BYTES)
+    return buf, path
 
 
 def main():
@@ -102,50 +202,26 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
-    ap.add_argument("--rng", default="numpy", choices=["numpy", "device", "mt"],
-                    help="numpy: reference jitter stream resident in HBM; mt: the same stream generated on "
-                         "the GPU inside every step (srt_mt19937_uniforms); device: Philox raygen")
+    ap.add_argument("--rng", default="mt", choices=["mt", "device"],
+                    help="mt: the reference's numpy stream generated on the GPU inside every step; device: Philox")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the latency / device-resident / roofline runs")
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--occupancy", type=int, default=0, help="experiment: kernel variant with this waves/SIMD bound")
+    ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
     ap.add_argument("--option", action="append", default=[],
                     help="experiment: srt_set_option KEY=VALUE before rendering (repeatable)")
-    ap.add_argument("--sync", action="store_true",
-                    help="one frame at a time (host waits for each frame) instead of pipelined frames")
-    ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
     ap.add_argument("--shard-of", type=int, default=0,
-                    help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job, to size the per-rank work "
-                         "of the multi-GPU run without the gather")
-    ap.add_argument("--rehearse-gather", action="store_true",
-                    help="diagnostic (1 GPU, with --shard-of N): run the N-rank step as one rank would, including "
-                         "the per-frame RCCL all-gather call (a 1-rank group) and row assembly, to size the host "
-                         "and stream overhead of the multi-GPU step")
+                    help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job (its per-frame work "
+                         "without the gather)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the N-rank path on a box with fewer GPUs (never used by the driver):
-    # SIGHTPY_BENCH_DEVICE=k puts every rank on GPU k, SIGHTPY_BENCH_BACKEND=gloo gathers on the host
-    dev = int(os.environ.get("SIGHTPY_BENCH_DEVICE", local))
-    backend = os.environ.get("SIGHTPY_BENCH_BACKEND", "nccl")
-    os.environ.setdefault("SIGHTPY_DEVICE", str(dev))
-    dist = None
-    if args.rehearse_gather and world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-    if world > 1 or args.rehearse_gather:
-        import torch
-        import torch.distributed as dist
-
-        torch.cuda.set_device(dev)
-        dist.init_process_group(backend)
+    os.environ["SIGHTPY_DEVICE"] = str(local)
 
     import scenes
     from sightpy import _backend as B, _native as N
-    from sightpy._shard import shard_rows, max_shard_rows, RowGather
 
     builder, W, H, depth, spp, label = CONFIGS[args.config]
     if args.spp:
@@ -154,173 +230,134 @@ def main():
         W, H = (int(v) for v in args.size.lower().split("x"))
     sc = getattr(scenes, builder)(W, H, depth)
     lib, ctx = B.context()
-    if args.occupancy:
-        N.check(lib, lib.srt_set_option(ctx, b"occupancy", args.occupancy))
-    if not args.sync:
-        # size every frame slot during the warmup (the first pipelined frame would allocate them)
-        N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))
+    id_path = None
+    if world > 1:
+        cid, id_path = comm_id_exchange(lib, N, rank, world)
+        N.check(lib, lib.srt_comm_init(ctx, world, rank, cid))
+    N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))  # size every frame slot during the warmup
     for kv in args.option:
         k, v = kv.split("=")
         N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
     B.upload(sc)
-    rows = shard_rows(H, world, rank) if world > 1 else np.arange(H)
-    if args.shard_of > 1 and world == 1:
-        rows = shard_rows(H, args.shard_of, 0)
-    npix = len(rows) * W
-    # resident inputs: jitter (reference stream, seed 0) in HBM
-    jit_dev = None
-    np.random.seed(0)
-    mt_state = np.random.get_state()
-    mt_key = np.ascontiguousarray(mt_state[1], dtype=np.uint32)
-    mt_key_out = np.empty(624, dtype=np.uint32)
-    mt_pos_out = ctypes.c_int32(0)
-    if args.rng == "mt" and world > 1:
-        raise SystemExit("--rng mt renders the full frame's stream; use it with --gpus 1")
-    if args.rng == "mt":
-        p = ctypes.c_void_p()
-        N.check(lib, lib.srt_device_alloc(ctx, spp * 4 * npix * 8, ctypes.byref(p)))
-        jit_dev = p
-    if args.rng == "numpy":
-        np.random.seed(0)
-        jit = np.random.rand(spp * 4 * H * W).reshape(spp, 4, H, W)[:, :, rows].reshape(spp, 4, npix)
-        jit = np.ascontiguousarray(jit)
-        p = ctypes.c_void_p()
-        N.check(lib, lib.srt_device_alloc(ctx, jit.nbytes, ctypes.byref(p)))
-        N.check(lib, lib.srt_memcpy(ctx, p, N.ptr(jit), jit.nbytes))
-        jit_dev = p
-        del jit
-    out_u8 = ctypes.c_void_p()
-    out_rgb = ctypes.c_void_p()
-    N.check(lib, lib.srt_device_alloc(ctx, 3 * npix, ctypes.byref(out_u8)))
-    N.check(lib, lib.srt_device_alloc(ctx, 3 * npix * 8, ctypes.byref(out_rgb)))
     cd = B.camera_desc(sc.camera)
-    rows32 = np.ascontiguousarray(rows, dtype=np.int32)
+    npix_full = W * H
+    flags = N.RENDER_SHARDED | N.RENDER_GATHER_RGB if world > 1 else 0
+    rows32 = None
+    if args.shard_of > 1 and world == 1:
+        from sightpy._shard import shard_rows
+
+        rows32 = np.ascontiguousarray(shard_rows(H, args.shard_of, 0), dtype=np.int32)
+        npix_full = len(rows32) * W  # the shard's outputs
+
+    # outputs: the whole frame in pinned host memory (rank 0), one pair of buffers per frame in flight
+    NOUT = 3
+    outs = []
+    for _ in range(NOUT if rank == 0 else 0):
+        pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full, ctypes.byref(pu)))
+        N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full * 8, ctypes.byref(pr)))
+        outs.append((pu, pr))
+
+    np.random.seed(0)
+    mt = N.MtState.from_numpy()
     a = N.RenderArgs()
-    a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, len(rows), 0
-    a.rows = N.ptr(rows32)
-    a.jitter = jit_dev
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, H, 0
+    a.rows = None
+    if rows32 is not None:
+        a.rows, a.n_rows = N.ptr(rows32), len(rows32)
+    a.jitter = None
+    a.mt = ctypes.pointer(mt) if args.rng == "mt" else None
     a.seed = 12345
-    a.out_rgb, a.out_srgb8, a.out_hit_id = out_rgb, out_u8, None
-
-    # Frames are pipelined: each step queues its frame on the library's stream (SRT_RENDER_ASYNC)
-    # and returns, so the host prepares frame k+1 while the GPU renders frame k; srt_render_finish
-    # at the end checks every frame's error flags.  With N ranks the frame's uint8 tile (written in
-    # place by k_resolve, double-buffered) is all-gathered over RCCL on torch's stream after the
-    # frame, overlapping the next frame's rendering.
-    pipelined = not args.sync and args.rng != "mt"
-    NTILE = int(os.environ.get("SIGHTPY_BENCH_NTILE", "5"))  # uint8 tiles in flight (gather ring)
-    tiles, done = None, [None] * NTILE
-    if dist is not None:
-        import torch
-
-        # each rank's uint8 tile, padded to the largest shard: the send buffer of the all-gather
-        tiles = [torch.zeros((max_shard_rows(H, world), W, 3), dtype=torch.uint8, device="cuda") for _ in range(NTILE)]
-        gather = RowGather(H, world, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
-        if world == 1:  # --rehearse-gather: rank 0's tile of an N-rank job through a 1-rank group
-            tiles = [torch.zeros((len(rows), W, 3), dtype=torch.uint8, device="cuda") for _ in range(NTILE)]
-            gather = RowGather(len(rows), 1, (W, 3), torch.uint8, "cuda" if backend == "nccl" else "cpu")
-    streams = {}
-
-    def frame_stream():
-        """torch handle of the stream the library queued its last frame on (pipelined frames
-        alternate between two streams)."""
-        import torch
-
-        sp = ctypes.c_void_p()
-        N.check(lib, lib.srt_stream(ctx, ctypes.byref(sp)))
-        if sp.value not in streams:
-            streams[sp.value] = torch.cuda.ExternalStream(sp.value, device=torch.device("cuda", dev))
-        return streams[sp.value]
-
+    a.out_hit_id = None
     frame = {"k": 0}
 
-    def step(st, async_ok=True):
-        if args.rng == "mt":
-            # the reference's stream (seed 0): spp x 4 x npix jitter + the sizing draw, on the GPU
-            N.check(lib, lib.srt_mt19937_uniforms(ctx, N.ptr(mt_key), int(mt_state[2]), spp * 4 * npix, 4 * npix,
-                                                  jit_dev, N.ptr(mt_key_out), ctypes.byref(mt_pos_out)))
-        i = frame["k"] % NTILE
+    def step(async_ok=True, st=None):
+        if outs:
+            u8, rgb = outs[frame["k"] % NOUT]
+            a.out_srgb8, a.out_rgb = u8, rgb
+        else:
+            a.out_srgb8 = a.out_rgb = None
         frame["k"] += 1
-        a.flags = N.RENDER_ASYNC if (pipelined and async_ok) else 0
-        if tiles is not None:
-            if done[i] is not None:
-                # the gather that read this tile NTILE frames ago must be done before this frame's
-                # resolve overwrites it (a host wait: by now it has long finished)
-                done[i].synchronize()
-            a.out_srgb8 = ctypes.c_void_p(tiles[i].data_ptr())
-        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
-        if tiles is not None:
-            import torch
-
-            cur = torch.cuda.current_stream()
-            cur.wait_stream(frame_stream())  # this frame's tile is complete
-            if backend == "nccl":
-                frame["image"] = gather(tiles[i])
-            else:
-                cur.synchronize()
-                frame["image"] = gather(tiles[i].cpu())
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            done[i] = ev
-
-    st = N.Stats()
-    for w in range(args.warmup):
-        step(st, async_ok=w > 0)  # the first frame runs synchronously (sizes the queues)
+        a.flags = flags | (N.RENDER_ASYNC if async_ok else 0)
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st) if st else None))
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
-            import torch
-            torch.cuda.synchronize()
+        N.check(lib, lib.srt_render_finish(ctx, None))
         N.check(lib, lib.srt_synchronize(ctx))
+        if world > 1:
+            N.check(lib, lib.srt_comm_barrier(ctx))
 
+    for w in range(args.warmup):
+        step(async_ok=w > 0)  # the first frame runs synchronously (sizes queues and rings)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(st)
-    barrier()
+        step()
+    last = N.Stats()
+    N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(last)))  # every frame in host memory, flags checked
+    if world > 1:
+        N.check(lib, lib.srt_comm_barrier(ctx))
     elapsed = time.perf_counter() - t0
-    N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(st)))  # error flags of every pipelined frame
-    # kernel durations (HIP events on the library's stream) of the same frame, rendered one at a
-    # time so that every frame's events can be read: the roofline's per-launch times
-    stats = []
-    for _ in range(max(1, min(args.steps, 10))):
-        s = N.Stats()
-        step(s, async_ok=False)
-        stats.append(s.as_dict())
-    barrier()
-    if dist is not None:
-        import torch
-
-        cdev = "cuda" if backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        rays_local = torch.tensor([stats[0]["total_rays"]], dtype=torch.float64, device=cdev)
-        dist.all_reduce(rays_local)
-        total_rays = float(rays_local.item())
+    last = last.as_dict()
+    vals = (ctypes.c_double * 2)(elapsed, float(last["total_rays"]))
+    if world > 1:
+        N.check(lib, lib.srt_comm_allreduce(ctx, vals, 1, 1))  # max elapsed over ranks
+        tot = (ctypes.c_double * 1)(float(last["total_rays"]))
+        N.check(lib, lib.srt_comm_allreduce(ctx, tot, 1, 0))  # rays of the frame, all ranks
+        elapsed, total_rays = vals[0], tot[0]
     else:
-        total_rays = float(stats[0]["total_rays"])
-
+        total_rays = float(last["total_rays"])
     ms_step = elapsed / args.steps * 1e3
     value = total_rays * args.steps / elapsed / 1e6
-    # roofline of the dominant kernel (depth-0 trace = raygen + trace; HIP events on its stream)
-    prim_ms = np.mean([s["ms_primary_kernel"] for s in stats])
-    trace_ms = np.mean([s["ms_trace_kernels"] for s in stats])
-    rpd = stats[0]["rays_per_depth"]
-    frame_path = stats[0]["kernel_path"] == "frame"
-    # the dominant kernel: k_primary (depth 0) on the wavefront path; k_frame (every ray of the
-    # pass) on the frame-kernel path used for branching scenes
-    prim_rays = stats[0]["total_rays"] if frame_path else rpd[0]
-    achieved = prim_rays * BYTES_PER_RAY / (prim_ms * 1e-3) / 1e9
-    family = stats[0]["total_rays"] * BYTES_PER_RAY / (trace_ms * 1e-3) / 1e9
-    # (PMC summaries are per launch of the full configuration: none for diagnostic shapes)
-    traffic_gb, traffic_src = (None, None) if (args.shard_of or args.size or args.spp) else \
-        pmc_traffic(args.config, "k_frame" if frame_path else "k_primary")
+
+    # ---- secondary figures --------------------------------------------------------------------
+    sec = {}
+    if not args.no_secondary:
+        # one synchronous frame, render() entry -> host memory (latency, not throughput)
+        lat = []
+        stats = []
+        for _ in range(3):
+            s = N.Stats()
+            t1 = time.perf_counter()
+            step(async_ok=False, st=s)
+            lat.append((time.perf_counter() - t1) * 1e3)
+            stats.append(s.as_dict())
+        sec["frame_latency_ms"] = round(float(np.median(lat)), 4)
+        sec["stats"] = stats
+        if world == 1 and rows32 is None:
+            # the round-1 headline form: jitter resident in HBM, outputs left in HBM
+            nj = spp * 4 * npix_full
+            jd, od, ud = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+            N.check(lib, lib.srt_device_alloc(ctx, nj * 8, ctypes.byref(jd)))
+            N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full * 8, ctypes.byref(od)))
+            N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full, ctypes.byref(ud)))
+            np.random.seed(0)
+            jh = np.random.rand(nj)
+            N.check(lib, lib.srt_memcpy(ctx, jd, N.ptr(jh), jh.nbytes))
+            del jh
+            r = N.RenderArgs()
+            r.spp, r.n_rows, r.jitter, r.seed, r.out_rgb, r.out_srgb8 = spp, H, jd, 12345, od, ud
+            r.flags = 0
+            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(r), None))
+            r.flags = N.RENDER_ASYNC
+            N.check(lib, lib.srt_synchronize(ctx))
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(r), None))
+            s = N.Stats()
+            N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(s)))
+            dt = time.perf_counter() - t1
+            sec["device_resident"] = {
+                "value": round(s.total_rays * args.steps / dt / 1e6, 3), "ms_per_step": round(dt / args.steps * 1e3, 4),
+                "what": "same frames with the jitter pre-resident in HBM (uploaded once) and the outputs left in HBM "
+                        "(the round-1 headline; excludes the in-step jitter generation and the host copies)"}
+            for p in (jd, od, ud):
+                lib.srt_device_free(ctx, p)
+
     if rank == 0:
         rec = {
-            "metric": "Mrays/sec (primary+secondary) at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
-            else "Mrays/sec (primary+secondary)",
+            "metric": "Mrays/sec (primary+secondary) + frame ms at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
+            else "Mrays/sec (primary+secondary) + frame ms",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -331,38 +368,61 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: %s; jitter = reference numpy stream seed 0 (%s)" % (label, args.rng),
+            "data": "synthetic: %s; jitter = the reference's numpy stream (seed 0, continued frame to frame) %s"
+                    % (label, "generated on the GPU inside each step" if args.rng == "mt" else "replaced by device Philox"),
             "config": {"workload": label, "width": W, "height": H, "max_ray_depth": depth, "spp": spp,
-                       "rays_per_frame": int(total_rays), "rays_per_depth_rank0": rpd,
-                       "shadow_rays_rank0": stats[0]["shadow_rays"], "kernel_path": stats[0]["kernel_path"],
-                       "chain_from_depth": stats[0]["chain_from"], "parallelism": ("row-band shards x%d" % world) if not args.shard_of
-                       else "diagnostic: rank 0 of %d row-band shards, %s" % (
-                           args.shard_of, "1-rank RCCL all-gather + assembly per frame" if args.rehearse_gather
-                           else "no gather"),
+                       "rays_per_frame": int(total_rays), "rays_per_depth_rank0": last["rays_per_depth"],
+                       "shadow_rays_rank0": last["shadow_rays"], "kernel_path": last["kernel_path"],
+                       "chain_from_depth": last["chain_from"],
+                       "parallelism": "row-band shards x%d, RCCL gather of uint8 + linear RGB to rank 0" % world
+                       if world > 1 else ("diagnostic: rank 0's rows of a %d-rank job, no gather" % args.shard_of
+                                          if rows32 is not None else "1 GPU"),
+                       "frame": "render() entry (scene resident) -> jitter stream on the GPU -> all samples and depths "
+                                "-> sRGB resolve -> uint8 + linear RGB (f64) in pinned host memory; frames pipelined",
                        "frame_ms": round(ms_step, 4)},
-            "roofline": {"bound": "hbm",
-                         "kernel": "k_frame (whole pass: every ray of every depth, one wave per 64-pixel tile)"
-                         if frame_path else "k_primary (depth 0: raygen + nearest hit + shading, fused)",
-                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None if traffic_gb is None else round(traffic_gb, 4),
-                         "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src,
-                         "algorithmic_GB_per_launch": round(prim_rays * BYTES_PER_RAY / 1e9, 4),
-                         "bytes_per_ray": BYTES_PER_RAY, "kernel_ms": round(float(prim_ms), 4),
-                         "all_trace_kernels": {"ms": round(float(trace_ms), 4), "achieved_GBs": round(family, 2),
-                                               "frac": round(family / HBM_PEAK_GBS, 4)}},
         }
+        if sec:
+            rec["config"]["frame_latency_ms"] = sec["frame_latency_ms"]
+            if "device_resident" in sec:
+                rec["device_resident"] = sec["device_resident"]
+            st0 = sec["stats"]
+            frame_path = st0[0]["kernel_path"] == "frame"
+            kname = "k_frame" if frame_path else "k_primary"
+            kms = float(np.mean([x["ms_primary_kernel"] for x in st0]))
+            traffic, src, krec = (None, None, None) if (args.size or args.spp or world > 1 or rows32 is not None) else \
+                pmc_traffic(args.config, kname)
+            from sightpy._shard import shard_rows
+
+            npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0)) * W
+            roof = {"kernel": kname, "kernel_ms": round(kms, 4), "unit": "GB/s", "peak": HBM_PEAK_GBS}
+            if st0[0]["passes"] == 1:
+                model = kernel_bytes_model(st0[0], spp, npix_rank, sc.camera.lens_radius != 0.0)
+                roof.update({"bound": "hbm", "achieved": round(model / (kms * 1e-3) / 1e9, 2),
+                             "frac": round(model / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "algorithmic_GB_per_launch": round(model / 1e9, 4),
+                             "bytes_model": kernel_bytes_model.__doc__.split("\n")[2 if frame_path else 1].strip()})
+            if traffic is not None:
+                roof["traffic"] = round(traffic, 4)
+                roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+                roof["traffic_source"] = src
+                if krec and krec.get("fp64_flop") and roof.get("kernel_ms"):
+                    tf = krec["fp64_flop"] / (kms * 1e-3) / 1e12
+                    roof["compute"] = {"fp64_TFLOPs": round(tf, 3), "peak": FP64_PEAK_TFS,
+                                       "frac": round(tf / FP64_PEAK_TFS, 4), "source": src}
+            rec["roofline"] = roof
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth, spp)
-        print(json.dumps(rec))
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    lib.srt_device_free(ctx, out_u8)
-    lib.srt_device_free(ctx, out_rgb)
-    if jit_dev is not None:
-        lib.srt_device_free(ctx, jit_dev)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        N.check(lib, lib.srt_comm_barrier(ctx))
+        if rank == 0 and id_path is not None:
+            try:
+                id_path.unlink()
+            except OSError:
+                pass
+    for pu, pr in outs:
+        lib.srt_host_free(ctx, pu)
+        lib.srt_host_free(ctx, pr)
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 3
+#define SRT_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------------------------ */
 #define SRT_OK 0
@@ -188,6 +188,13 @@ typedef struct srt_camera {
     double focal_distance;
 } srt_camera;
 
+/* numpy's legacy global RandomState (np.random.get_state(): MT19937 key window and position) */
+typedef struct srt_mt_state {
+    uint32_t key[624];
+    int32_t pos; /* 0..624 */
+    int32_t reserved;
+} srt_mt_state;
+
 typedef struct srt_render_args {
     int32_t spp;          /* samples traced by this call */
     int32_t sample_base;  /* global index of the first sample (RNG key) */
@@ -195,8 +202,16 @@ typedef struct srt_render_args {
     int32_t batch_spp;    /* samples per device pass (0 = fit to the HBM budget) */
     const int32_t* rows;  /* [n_rows] global row index of each local row; NULL = 0..n_rows-1 */
     const double* jitter; /* [spp][4][n_rows*width] uniforms (x-jitter, y-jitter, r, phi) in
-                             numpy's draw order, or NULL = device Philox keyed by (seed, pixel,
-                             sample) */
+                             numpy's draw order, or NULL (then `mt`, else device Philox keyed by
+                             (seed, pixel, sample)) */
+    srt_mt_state* mt;     /* jitter == NULL, mt != NULL: the jitter is numpy's legacy rand stream
+                             from *mt exactly as Scene.render draws it (Camera.get_ray per sample,
+                             camera.py:56-64, then one more get_ray for sizing, scene.py:81: that is
+                             spp*4*width*height doubles of which a shard reads its rows, then
+                             4*width*height skipped), generated on the device (rt_mt.h); *mt is
+                             advanced past them.  Consecutive asynchronous frames that pass the same
+                             `mt` continue the stream on the device; *mt is written by
+                             srt_render_finish */
     uint64_t seed;        /* device RNG key (jitter when jitter == NULL, Monte-Carlo shading) */
     double* out_rgb;      /* [3][n_rows*width] linear RGB averaged over spp, or NULL */
     uint8_t* out_srgb8;   /* [n_rows*width][3] resolved image, or NULL */
@@ -205,13 +220,23 @@ typedef struct srt_render_args {
     int32_t reserved;
 } srt_render_args;
 
-/* SRT_RENDER_ASYNC: queue the frame on the context's stream and return at once (jitter and outputs
- * must be device memory or NULL; `stats` is not written).  Consecutive asynchronous frames of the
- * same shape pipeline back to back without host round trips; srt_render_finish waits for them,
- * checks their error flags and returns the last one's stats.  Any other call on the context first
- * finishes pending frames.  (No reference counterpart: Scene.render is synchronous; this serves
- * frame sequences such as create_animation and the multi-GPU frame loop.) */
+/* SRT_RENDER_ASYNC: queue the frame on the context's stream and return at once (jitter must be
+ * device memory or NULL, outputs device memory, pinned host memory from srt_host_alloc, or NULL;
+ * `stats` is not written).  Consecutive asynchronous frames of the same shape pipeline back to back
+ * without host round trips; srt_render_finish waits for them, checks their error flags and returns
+ * the last one's stats.  Any other call on the context first finishes pending frames.  (No
+ * reference counterpart: Scene.render is synchronous; this serves frame sequences such as
+ * create_animation and the multi-GPU frame loop.) */
 #define SRT_RENDER_ASYNC 1
+/* SRT_RENDER_SHARDED: the context's communicator (srt_comm_init / srt_comm_init_all) splits the
+ * frame: this rank renders the rows {y : (y / 8) % nranks == rank} (8-row bands dealt round-robin,
+ * which balances cheap sky rows against reflective floor rows; rows / n_rows are ignored) and the
+ * uint8 and linear-RGB tiles are gathered over RCCL to rank 0, whose out_srgb8 / out_rgb receive the
+ * whole frame ([height][width][3], [3][height*width]); the other ranks' outputs are not written.
+ * Replaces the reference's multiprocessing.Pool over samples (scene.py:80-116). */
+#define SRT_RENDER_SHARDED 2
+/* with SRT_RENDER_SHARDED: gather the linear RGB as well (every rank passes the same flags) */
+#define SRT_RENDER_GATHER_RGB 4
 
 #define SRT_MAX_DEPTHS 64
 typedef struct srt_stats {
@@ -273,6 +298,29 @@ int srt_primary_rays(srt_ctx* ctx, const srt_camera* cam, const double* jitter /
  * parity-mode renders need no host RNG and no host-to-device jitter copy. */
 int srt_mt19937_uniforms(srt_ctx* ctx, const uint32_t* key, int32_t pos, int64_t n_out, int64_t n_skip,
                          double* out, uint32_t* key_out, int32_t* pos_out);
+
+/* ---- multi-GPU: row-band shards + RCCL gather over xGMI -------------------------
+ * One context per GPU.  Several processes (one per GPU): rank 0 makes an id with
+ * srt_comm_unique_id, every rank passes it to srt_comm_init.  One process driving several GPUs:
+ * srt_comm_init_all creates one context per device with one communicator (ncclCommInitAll), and
+ * srt_render_group renders a frame on all of them (each its shard, SRT_RENDER_SHARDED) and gathers
+ * it to the first. */
+#define SRT_COMM_ID_BYTES 128
+int srt_comm_unique_id(uint8_t* id /* [SRT_COMM_ID_BYTES] */);
+int srt_comm_init(srt_ctx* ctx, int nranks, int rank, const uint8_t* id);
+int srt_comm_init_all(int ndev, const int* devs, srt_ctx** ctxs /* [ndev], out */);
+int srt_comm_rank(srt_ctx* ctx, int* nranks, int* rank);
+/* frame of srt_render on every context of an srt_comm_init_all group; args of rank 0 (its outputs
+ * receive the frame), stats of rank 0 plus total_rays / rays_per_depth / shadow_rays summed */
+int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);
+/* collectives over the communicator for callers' bookkeeping (host values, blocking):
+ * op 0 = sum, 1 = max; n doubles */
+int srt_comm_allreduce(srt_ctx* ctx, double* vals, int n, int op);
+int srt_comm_barrier(srt_ctx* ctx);
+
+/* Pinned host memory (outputs of asynchronous frames are copied into it by the frame's stream). */
+int srt_host_alloc(srt_ctx* ctx, int64_t bytes, void** out);
+int srt_host_free(srt_ctx* ctx, void* ptr);
 /* Device memory helpers for callers that keep inputs resident in HBM (bench, multi-GPU). */
 int srt_device_alloc(srt_ctx* ctx, int64_t bytes, void** out);
 int srt_device_free(srt_ctx* ctx, void* ptr);

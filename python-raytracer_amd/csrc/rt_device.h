@@ -1094,6 +1094,14 @@ RT_HD void shade_hit(const SceneView& S, int cid, int mi, const Ray& r, double t
 // RNG stream of the Monte-Carlo refraction pick / diffuse children of a ray
 RT_HD uint32_t child_path(uint32_t path, uint32_t slot, uint32_t round) { return mix32(path, slot + 4096u * round); }
 
+// ---- row-band shards of a frame over ranks (SRT_RENDER_SHARDED) ---------------------------------
+// Rank q of n renders the rows {y : (y / SHARD_BAND) % n == q}: bands of 8 rows dealt round-robin
+// (the reference parallelises over samples instead, scene.py:80-116).  Its local row i holds global
+// row ((i / SHARD_BAND) * n + q) * SHARD_BAND + i % SHARD_BAND.
+constexpr int SHARD_BAND = 8;
+RT_HD int shard_of_row(int64_t y, int n) { return (int)((y / SHARD_BAND) % n); }
+RT_HD int64_t shard_local_row(int64_t y, int n) { return (y / ((int64_t)SHARD_BAND * n)) * SHARD_BAND + y % SHARD_BAND; }
+
 // sRGB_linear_to_sRGB + clip + uint8 for one pixel (colour_functions.py:4-18, scene.py:125-140)
 RT_HD void resolve_pixel(double r, double g, double b, double& orr, double& og, double& ob, uint8_t px[3]) {
     double c[3] = {r, g, b}, e[3];

@@ -298,6 +298,14 @@ void hc_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out) {
 }
 uint32_t hc_mix32(uint32_t h, uint32_t v) { return mix32(h, v); }
 
+// row-band shard map of the sharded render (rt_device.h): owner rank and local row of global row y
+void hc_shard_map(int64_t H, int n, int32_t* owner, int64_t* local) {
+    for (int64_t y = 0; y < H; ++y) {
+        owner[y] = shard_of_row(y, n);
+        local[y] = shard_local_row(y, n);
+    }
+}
+
 // numpy legacy rand stream by the segmented jump-ahead scheme of rt_mt.h, run serially
 int hc_mt_uniforms(const uint32_t* key, int pos, int64_t n_out, int64_t n_skip, double* out, uint32_t* key_out,
                    int* pos_out) {

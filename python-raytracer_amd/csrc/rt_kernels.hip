@@ -18,6 +18,7 @@
 // present in a wave so each material's parameters are wave-uniform too.  Children are appended
 // with one block-wide exclusive scan and one atomicAdd per block.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -56,7 +57,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 784;
+constexpr size_t TRACE_PARAMS_BYTES = 800;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
@@ -86,7 +87,9 @@ struct TraceParams {
     int64_t n_primary;
     srt_camera cam;
     const int32_t* rows;
-    const double* jitter;  // [spp][4][npix] (device) or null
+    const double* jitter;  // [spp][4][jit_plane] (device) or null
+    int64_t jit_plane;     // doubles per jitter plane: npix, or width*height when jit_global
+    int jit_global;        // 1: jitter indexed by the global pixel (the whole frame's numpy stream)
     int sample_base;
     int spp;           // samples of this pass (k_primary)
     int spt;           // samples per thread: k_primary item i = (pixel i % npix, samples [g*spt, g*spt+spt)),
@@ -231,10 +234,11 @@ __device__ __forceinline__ double mc_uniform(const TraceParams& P, const Ray& r,
 __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, uint32_t p, uint32_t gpix,
                                                  double j[4]) {
     if (P.jitter) {
-        const double* base = P.jitter + (int64_t)s * 4 * P.npix + p;
-        j[0] = base[0]; j[1] = base[P.npix];
+        const int64_t plane = P.jit_plane;
+        const double* base = P.jitter + (int64_t)s * 4 * plane + (P.jit_global ? gpix : p);
+        j[0] = base[0]; j[1] = base[plane];
         // the lens-disk pair is read only by a thin-lens camera (pinhole: primary_ray skips it)
-        if (P.cam.lens_radius != 0.0) { j[2] = base[2 * P.npix]; j[3] = base[3 * P.npix]; }
+        if (P.cam.lens_radius != 0.0) { j[2] = base[2 * plane]; j[3] = base[3 * plane]; }
     } else {
         Rng g;
         g.init(P.seed, gpix, (uint32_t)(P.sample_base + s), 0xCA3E0000u);
@@ -827,6 +831,42 @@ __global__ __launch_bounds__(BLOCK) void k_primary_rays(srt_camera cam, const do
     }
 }
 
+// ---- row-band shards (SRT_RENDER_SHARDED, rt_device.h shard_of_row) -----------------------------
+// Rank 0 gathers every rank's tiles (RCCL) and k_assemble writes them into the frame.
+constexpr int BAND = SHARD_BAND;
+constexpr int MAX_RANKS = 64;
+struct GatherTiles {
+    const uint8_t* u8[MAX_RANKS];  // [rows_q][W][3]
+    const double* rgb[MAX_RANKS];  // [3][rows_q * W]
+    int64_t npix[MAX_RANKS];       // rows_q * W
+};
+
+__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t W, int64_t H, uint8_t* u8,
+                                                   double* rgb) {
+    const int64_t n = W * H;
+    for (int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x; g < n; g += (int64_t)gridDim.x * BLOCK) {
+        const int64_t y = g / W, x = g - y * W;
+        const int q = shard_of_row(y, nranks);
+        const int64_t l = shard_local_row(y, nranks) * W + x;
+        if (u8) {
+            const uint8_t* s = T.u8[q] + 3 * l;
+            u8[3 * g] = s[0]; u8[3 * g + 1] = s[1]; u8[3 * g + 2] = s[2];
+        }
+        if (rgb) {
+            const double* s = T.rgb[q];
+            const int64_t np = T.npix[q];
+            rgb[g] = s[l]; rgb[n + g] = s[np + l]; rgb[2 * n + g] = s[2 * np + l];
+        }
+    }
+}
+
+std::vector<int32_t> band_rows(int64_t H, int n, int q) {
+    std::vector<int32_t> r;
+    for (int64_t y = 0; y < H; ++y)
+        if (shard_of_row(y, n) == q) r.push_back((int32_t)y);
+    return r;
+}
+
 template <typename T>
 hipError_t dalloc(T** p, int64_t count) {
     return hipMalloc((void**)p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
@@ -1021,6 +1061,8 @@ struct FramePlan {
     bool frame = false;  // rendered by k_frame (counts are totals, not queue fills)
     int chain_from = 0;  // > 0: k_trace at this depth runs in chain mode and no deeper kernel is launched
     int64_t npix = 0;
+    int64_t W = 0, H = 0;  // frame shape (a shard renders npix of W * H)
+    bool sharded = false, gather_rgb = false, use_mt = false;
     int spp = 0, batch = 0, npass = 0, dcap = 0, nev = 0;
     int64_t cnt_words = 0, pass_words = 0;
 };
@@ -1063,6 +1105,25 @@ struct FrameSlot {
     std::vector<hipEvent_t> ev;
     uint32_t* host = nullptr;  // pinned: per-pass counters/flags, shadow count
     int64_t host_words = 0;
+    // SRT_RENDER_SHARDED on rank 0: every rank's tiles (padded to the largest shard) and the frame
+    uint8_t* g_u8 = nullptr;
+    int64_t g_u8_cap = 0;
+    double* g_rgb = nullptr;
+    int64_t g_rgb_cap = 0;
+    uint8_t* full_u8 = nullptr;
+    int64_t full_u8_cap = 0;
+    double* full_rgb = nullptr;
+    int64_t full_rgb_cap = 0;
+    // the frame's gather (srt_render_group posts it for all its contexts in one RCCL group)
+    struct Gather {
+        bool on = false;
+        int64_t W = 0, H = 0, npix = 0, maxpix = 0;
+        bool want_u8 = false, want_rgb = false;
+        uint8_t* dst_u8 = nullptr;  // where k_assemble writes (caller's device buffer or full_u8)
+        double* dst_rgb = nullptr;
+        uint8_t* host_u8 = nullptr;  // caller's host buffer (copied after k_assemble) or null
+        double* host_rgb = nullptr;
+    } gather;
     // counts/flags/shadow are zeroed by the kernels that consume them (k_pass_end, k_resolve); a
     // frame that did not complete leaves them dirty and the next one clears them first
     bool dirty = true;
@@ -1116,6 +1177,18 @@ struct srt_ctx {
     int last_slot = 0;      // slot of the last asynchronous frame (its stats are reported)
     int async_pending = 0;  // asynchronous frames in flight (all slots)
     srt_stats async_stats{};
+    // numpy-stream jitter generated on the device (render args `mt`): the state after the last
+    // queued frame stays on the device (mt dump window) while consecutive asynchronous frames pass the
+    // same host state, which srt_render_finish then writes
+    srt_mt_state* mt_chain = nullptr;
+    int mt_pos = 0;
+    hipEvent_t mt_done = nullptr;  // recorded after the last frame's stream generation
+    bool mt_tables = false;
+    // multi-GPU (srt_comm_init / srt_comm_init_all)
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    bool defer_gather = false;  // srt_render_group posts the gathers of all its contexts in one group
+    double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
 namespace {
@@ -1214,6 +1287,26 @@ bool is_device_ptr(const void* p) {
     return a.type == hipMemoryTypeDevice;
 }
 
+// 0: null, 1: device memory, 2: pinned host memory (hipHostMalloc / registered), 3: other host memory
+int ptr_kind(const void* p) {
+    if (!p) return 0;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 3;
+    }
+    if (a.type == hipMemoryTypeDevice) return 1;
+    if (a.type == hipMemoryTypeHost) return 2;
+    return 3;
+}
+
+#define NCCL_TRY(expr)                                                                          \
+    do {                                                                                        \
+        ncclResult_t _r = (expr);                                                               \
+        if (_r != ncclSuccess)                                                                  \
+            return fail(SRT_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r));      \
+    } while (0)
+
 int check_flags(uint32_t f0) {
     if (f0 & ERR_INDEX)
         return fail(SRT_ERR_INDEX, "index out of bounds in a texture/table lookup (reference raises IndexError)");
@@ -1279,6 +1372,44 @@ int64_t depth_total(const uint32_t* cnt, int64_t seg) {
 }  // namespace
 
 namespace {
+
+// ---- numpy's stream on the device (rt_mt.h): scratch c->mt = jump tables | key 0 | key 1 | dump ----
+constexpr int64_t MT_NTAB = 31 * rtmt::N;
+uint32_t* mt_key0(srt_ctx* c) { return c->mt + MT_NTAB; }
+uint32_t* mt_dump(srt_ctx* c) { return c->mt + MT_NTAB + 2 * rtmt::N; }
+
+int mt_ensure(srt_ctx* c) {
+    if (c->mt) return SRT_OK;
+    HIP_TRY(dalloc(&c->mt, MT_NTAB + 3 * rtmt::N));
+    HIP_TRY(hipMemcpy(c->mt, rtmt::tables_flat(), MT_NTAB * 4, hipMemcpyHostToDevice));
+    return SRT_OK;
+}
+
+// Queue on `st`: from the key window in mt_key0 at position `pos`, n_out doubles into `out` (device)
+// and n_skip more draws; the window holding the last consumed word goes to mt_dump.  Returns the
+// numpy position of that window in *final_pos.
+int mt_launch(srt_ctx* c, hipStream_t st, int pos, int64_t n_out, int64_t n_skip, double* out, int* final_pos) {
+    uint32_t* keys[2] = {c->mt + MT_NTAB, c->mt + MT_NTAB + rtmt::N};
+    const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
+    for (size_t r = 0; r < plan.rounds.size(); ++r) {
+        const rtmt::Round& R = plan.rounds[r];
+        MtArgs A{};
+        A.key = keys[r & 1];
+        A.tab = c->mt;
+        A.out = out;
+        A.chain_dst = R.chain ? keys[(r + 1) & 1] : nullptr;
+        A.dump_dst = R.dump_at >= 0 ? mt_dump(c) : nullptr;
+        A.words = R.words;
+        A.double_base = R.double_base;
+        A.n_out = n_out;
+        A.dump_at = R.dump_at;
+        A.pos = R.pos;
+        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), 0, st, A);
+        HIP_TRY(hipGetLastError());
+    }
+    *final_pos = plan.final_pos;
+    return SRT_OK;
+}
 
 // Read back a completed frame (its stream has been synchronised): error/overflow flags OR-ed over
 // every pass (and every asynchronous frame since the last synchronisation point), per-depth counts
@@ -1358,7 +1489,7 @@ void free_slot(FrameSlot& f) {
     (void)hipStreamSynchronize(f.stream);
     free_list(f.queue_bufs);
     free_list(f.ring_bufs);
-    void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow};
+    void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -1379,6 +1510,11 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     for (FrameSlot& f : c->slots)
         if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
     c->async_pending = 0;
+    if (c->mt_chain) {  // numpy's state after the last asynchronous frame's draws
+        HIP_TRY(hipMemcpy(c->mt_chain->key, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost));
+        c->mt_chain->pos = c->mt_pos;
+        c->mt_chain = nullptr;
+    }
     int first_err = SRT_OK;
     bool overflow = false;
     srt_stats last{};
@@ -1410,6 +1546,63 @@ int finish_async(srt_ctx* c, srt_stats* st) {
                                     "off) during an asynchronous frame: render that frame again");
     c->async_stats = last;
     if (st) *st = last;
+    return SRT_OK;
+}
+
+int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) {
+    return (int64_t)band_rows(G.H, nranks, q).size() * G.W;
+}
+
+// Post this rank's part of the frame's gather on its stream (inside an RCCL group): rank 0 receives
+// every other rank's uint8 (and linear-RGB) tile, the others send theirs.
+int gather_post(srt_ctx* c) {
+    const FrameSlot::Gather& G = c->f->gather;
+    if (!G.on || c->nranks == 1) return SRT_OK;
+    hipStream_t st = c->f->stream;
+    if (c->rank == 0) {
+        for (int q = 1; q < c->nranks; ++q) {
+            const int64_t np = shard_npix(G, c->nranks, q);
+            NCCL_TRY(ncclRecv(c->f->g_u8 + (int64_t)q * G.maxpix * 3, (size_t)(3 * np), ncclUint8, q, c->comm, st));
+            if (G.want_rgb)
+                NCCL_TRY(ncclRecv(c->f->g_rgb + (int64_t)q * G.maxpix * 3, (size_t)(3 * np), ncclFloat64, q, c->comm, st));
+        }
+    } else {
+        NCCL_TRY(ncclSend(c->f->u8, (size_t)(3 * G.npix), ncclUint8, 0, c->comm, st));
+        if (G.want_rgb) NCCL_TRY(ncclSend(c->f->rgb, (size_t)(3 * G.npix), ncclFloat64, 0, c->comm, st));
+    }
+    return SRT_OK;
+}
+
+int gather_finish(srt_ctx* c);
+
+// The frame's gather on its own (one rank per process): post it in a group, assemble on rank 0.
+int gather_frame(srt_ctx* c) {
+    if (c->nranks > 1) {
+        NCCL_TRY(ncclGroupStart());
+        int rc = gather_post(c);
+        NCCL_TRY(ncclGroupEnd());
+        if (rc) return rc;
+    }
+    return gather_finish(c);
+}
+
+// Rank 0, after the gather: the tiles into the frame, then to the caller's host buffers if any.
+int gather_finish(srt_ctx* c) {
+    const FrameSlot::Gather& G = c->f->gather;
+    if (!G.on || c->rank != 0) return SRT_OK;
+    GatherTiles T{};
+    for (int q = 0; q < c->nranks; ++q) {
+        T.u8[q] = q == 0 ? c->f->u8 : c->f->g_u8 + (int64_t)q * G.maxpix * 3;
+        T.rgb[q] = q == 0 ? c->f->rgb : c->f->g_rgb + (int64_t)q * G.maxpix * 3;
+        T.npix[q] = shard_npix(G, c->nranks, q);
+    }
+    hipStream_t st = c->f->stream;
+    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.W, G.H,
+                       G.want_u8 ? G.dst_u8 : nullptr, G.want_rgb ? G.dst_rgb : nullptr);
+    HIP_TRY(hipGetLastError());
+    if (G.host_u8) HIP_TRY(hipMemcpyAsync(G.host_u8, G.dst_u8, (size_t)3 * G.W * G.H, hipMemcpyDeviceToHost, st));
+    if (G.host_rgb)
+        HIP_TRY(hipMemcpyAsync(G.host_rgb, G.dst_rgb, (size_t)3 * G.W * G.H * 8, hipMemcpyDeviceToHost, st));
     return SRT_OK;
 }
 
@@ -1454,9 +1647,12 @@ int srt_create(int device, srt_ctx** out) {
 int srt_destroy(srt_ctx* c) {
     if (!c) return SRT_OK;
     (void)hipSetDevice(c->device);
+    (void)finish_async(c, nullptr);
     for (FrameSlot& f : c->slots) free_slot(f);
     free_list(c->scene_bufs);
-    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels};
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->mt_done) (void)hipEventDestroy(c->mt_done);
+    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     delete c;
@@ -1603,30 +1799,51 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
-    if (a->spp <= 0 || cam->width <= 0 || cam->height <= 0 || a->n_rows <= 0 || !cam->xs || !cam->ys)
-        return fail(SRT_ERR_ARG, "spp, width, height, n_rows must be positive and xs/ys set");
-    if (a->flags & ~SRT_RENDER_ASYNC) return fail(SRT_ERR_ARG, "unknown render flag");
+    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB))
+        return fail(SRT_ERR_ARG, "unknown render flag");
     const bool async = (a->flags & SRT_RENDER_ASYNC) != 0;
+    const bool sharded = (a->flags & SRT_RENDER_SHARDED) != 0;
+    if (a->spp <= 0 || cam->width <= 0 || cam->height <= 0 || (!sharded && a->n_rows <= 0) || !cam->xs || !cam->ys)
+        return fail(SRT_ERR_ARG, "spp, width, height, n_rows must be positive and xs/ys set");
+    if (a->jitter && a->mt) return fail(SRT_ERR_ARG, "jitter and mt are exclusive");
+    const bool use_mt = a->mt != nullptr;
+    if (use_mt && (a->mt->pos < 0 || a->mt->pos > rtmt::N)) return fail(SRT_ERR_ARG, "bad numpy RNG position");
+    // rows of this call
     std::vector<int32_t> rows_h;
-    if (a->rows) {
+    const int32_t* rows_src = nullptr;
+    int n_rows = a->n_rows;
+    if (sharded) {
+        if (c->nranks > MAX_RANKS) return fail(SRT_ERR_ARG, "too many ranks");
+        if (cam->height < (int64_t)BAND * c->nranks)
+            return fail(SRT_ERR_ARG, "a sharded frame needs at least 8 rows per rank");
+        if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
+        rows_h = band_rows(cam->height, c->nranks, c->rank);
+        n_rows = (int)rows_h.size();
+        rows_src = rows_h.data();
+    } else if (a->rows) {
         if (is_device_ptr(a->rows)) return fail(SRT_ERR_ARG, "rows must be host memory");
         for (int k = 0; k < a->n_rows; ++k)
             if (a->rows[k] < 0 || a->rows[k] >= cam->height) return fail(SRT_ERR_ARG, "row index out of range");
+        rows_src = a->rows;
     } else {
         if (a->n_rows > cam->height) return fail(SRT_ERR_ARG, "n_rows > height");
         rows_h.resize(a->n_rows);
         for (int k = 0; k < a->n_rows; ++k) rows_h[k] = k;
+        rows_src = rows_h.data();
     }
     HIP_TRY(hipSetDevice(c->device));
-    const int64_t W = cam->width;
-    const int64_t npix = (int64_t)a->n_rows * W;
-    if (npix >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "image too large");
-    const bool jit_dev = is_device_ptr(a->jitter);
-    const bool hit_dev = is_device_ptr(a->out_hit_id);
-    const bool rgb_dev = is_device_ptr(a->out_rgb), u8_dev = is_device_ptr(a->out_srgb8);
-    if (async && ((a->jitter && !jit_dev) || (a->out_hit_id && !hit_dev) || (a->out_rgb && !rgb_dev) ||
-                  (a->out_srgb8 && !u8_dev)))
-        return fail(SRT_ERR_ARG, "an asynchronous render takes device (or NULL) jitter and outputs");
+    const int64_t W = cam->width, Hf = cam->height;
+    const int64_t npix = (int64_t)n_rows * W;
+    if (W * Hf >= ((int64_t)1 << 31)) return fail(SRT_ERR_ARG, "image too large");
+    const int jk = ptr_kind(a->jitter), hk = ptr_kind(a->out_hit_id);
+    const int rk = ptr_kind(a->out_rgb), uk = ptr_kind(a->out_srgb8);
+    const bool jit_dev = jk == 1, hit_dev = hk == 1, rgb_dev = rk == 1, u8_dev = uk == 1;
+    if (async && (jk >= 2 || hk >= 2 || rk == 3 || uk == 3))
+        return fail(SRT_ERR_ARG, "an asynchronous render takes device (or NULL) jitter and hit ids, and device or "
+                                 "pinned host (srt_host_alloc) outputs");
+    // outputs written by this rank: a shard's tiles stay on the device (the gather reads them); rank 0
+    // of a sharded frame writes the whole frame to the caller's buffers after the gather
+    const bool gather_rgb = sharded && (a->flags & SRT_RENDER_GATHER_RGB) != 0;
     int rc;
     // samples per pass: both queues must hold spp_pass * npix * fanout rays
     const int64_t per_sample = npix * c->fanout;
@@ -1635,8 +1852,15 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                                  : (int)std::max<int64_t>(1, std::min<int64_t>(1 << 20, budget_rays / per_sample));
     batch = std::min(batch, a->spp);
     while (batch > 1 && (int64_t)batch * npix * c->fanout >= ((int64_t)1 << 32) - 1) batch /= 2;
+    // the numpy stream of a pass (its samples of the whole frame) is generated into the jitter buffer
+    if (use_mt) while (batch > 1 && (int64_t)batch * 4 * W * Hf * 8 > ((int64_t)8 << 30)) batch /= 2;
     FramePlan F;
     F.npix = npix;
+    F.W = W;
+    F.H = Hf;
+    F.sharded = sharded;
+    F.gather_rgb = gather_rgb;
+    F.use_mt = use_mt;
     F.spp = a->spp;
     F.batch = batch;
     F.npass = (a->spp + batch - 1) / batch;
@@ -1659,15 +1883,22 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if ((rc = ensure_slot(f))) return rc;
         c->f = &f;
     }
+    const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * W * Hf : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
+    const int64_t maxpix = sharded ? (int64_t)band_rows(Hf, c->nranks, 0).size() * W : 0;  // rank 0 has the most rows
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
     // for them (and reports their errors)
     if (async && c->async_pending > 0) {
         const FramePlan& pp = c->f->pending ? c->f->plan : c->slots[c->last_slot].plan;
-        const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && a->n_rows <= c->cam_cap[2] &&
+        const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && n_rows <= c->cam_cap[2] &&
                           3 * npix <= c->f->fb_cap && 3 * npix <= c->f->rgb_cap && 3 * npix <= c->f->u8_cap &&
+                          jit_doubles <= c->f->jit_cap &&
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
                           (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
-                          F.frame == pp.frame && F.chain_from == pp.chain_from &&
+                          F.frame == pp.frame && F.chain_from == pp.chain_from && F.W == pp.W && F.H == pp.H &&
+                          F.sharded == pp.sharded && F.gather_rgb == pp.gather_rgb && F.use_mt == pp.use_mt &&
+                          (!sharded || c->rank != 0 ||
+                           (c->f->g_u8_cap >= c->nranks * maxpix * 3 && c->f->full_u8_cap >= 3 * W * Hf &&
+                            (!gather_rgb || (c->f->g_rgb_cap >= c->nranks * maxpix * 3 && c->f->full_rgb_cap >= 3 * W * Hf)))) &&
                           (int)c->f->ev.size() >= F.npass * F.nev && c->f->host_words >= F.npass * F.pass_words + 2;
         if (!same) {
             FrameSlot* keep = c->f;
@@ -1679,7 +1910,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         const void* old[3] = {c->xs, c->ys, c->rows};
         if ((rc = ensure_buf(&c->xs, c->cam_cap[0], W))) return rc;
         if ((rc = ensure_buf(&c->ys, c->cam_cap[1], cam->height))) return rc;
-        if ((rc = ensure_buf(&c->rows, c->cam_cap[2], a->n_rows))) return rc;
+        if ((rc = ensure_buf(&c->rows, c->cam_cap[2], n_rows))) return rc;
         const void* now[3] = {c->xs, c->ys, c->rows};
         for (int k = 0; k < 3; ++k)
             if (old[k] != now[k]) c->cam_host[k].clear();
@@ -1687,8 +1918,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // camera tables: uploaded only when they change (a render loop re-sends the same ones)
     if ((rc = upload_if_changed(c, c->xs, c->cam_host[0], cam->xs, (size_t)W * 8))) return rc;
     if ((rc = upload_if_changed(c, c->ys, c->cam_host[1], cam->ys, (size_t)cam->height * 8))) return rc;
-    if ((rc = upload_if_changed(c, c->rows, c->cam_host[2], a->rows ? a->rows : rows_h.data(), (size_t)a->n_rows * 4)))
-        return rc;
+    if ((rc = upload_if_changed(c, c->rows, c->cam_host[2], rows_src, (size_t)n_rows * 4))) return rc;
+    if (use_mt && (rc = mt_ensure(c))) return rc;
     // per-slot buffers of this frame shape (for an asynchronous frame also those of the other slot
     // while it is idle, so that the pipeline's first frame on it allocates nothing)
     auto ensure_frame = [&](FrameSlot& fs) -> int {
@@ -1698,8 +1929,14 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!r) r = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
-        if (!r && a->jitter && !jit_dev) r = ensure_buf(&c->f->jit, c->f->jit_cap, (int64_t)batch * 4 * npix);
+        if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
         if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
+        if (!r && sharded && c->rank == 0) {
+            r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, c->nranks * maxpix * 3);
+            if (!r) r = ensure_buf(&c->f->full_u8, c->f->full_u8_cap, 3 * W * Hf);
+            if (!r && gather_rgb) r = ensure_buf(&c->f->g_rgb, c->f->g_rgb_cap, c->nranks * maxpix * 3);
+            if (!r && gather_rgb) r = ensure_buf(&c->f->full_rgb, c->f->full_rgb_cap, 3 * W * Hf);
+        }
         if (!r) r = F.frame ? ensure_ring(c, (int64_t)FRAME_BLOCK * (c->fanout + 2) * 2)
                             : ensure_queues(c, (int64_t)batch * npix * c->fanout);
         if (!r && (int)c->f->ev.size() < F.npass * F.nev) {
@@ -1733,12 +1970,16 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 if ((rc = ensure_frame(other))) return rc;
             }
     }
+    if (use_mt && !c->mt_done) HIP_TRY(hipEventCreateWithFlags(&c->mt_done, hipEventDisableTiming));
     const Variant& V = pick_variant(c->mats);
-    // outputs already in device memory are written in place by k_resolve (no copies)
-    double* res_rgb = a->out_rgb ? (rgb_dev ? a->out_rgb : c->f->rgb) : nullptr;
-    uint8_t* res_u8 = a->out_srgb8 ? (u8_dev ? a->out_srgb8 : c->f->u8) : nullptr;
+    // resolve targets: outputs already in device memory are written in place by k_resolve (no copies);
+    // a shard resolves into its slot tiles (gathered afterwards)
+    double* res_rgb = sharded ? (gather_rgb ? c->f->rgb : nullptr) : a->out_rgb ? (rgb_dev ? a->out_rgb : c->f->rgb) : nullptr;
+    uint8_t* res_u8 = sharded ? c->f->u8 : a->out_srgb8 ? (u8_dev ? a->out_srgb8 : c->f->u8) : nullptr;
     // only the depths this frame can reach are handed back and cleared per pass
     const int64_t used_words = std::min<int64_t>(F.cnt_words, (int64_t)(F.dcap + 2) * NSHARD);
+    // the numpy stream continues on the device from the previous asynchronous frame (same `mt`)
+    const bool mt_chained = use_mt && async && c->async_pending > 0 && c->mt_chain == a->mt;
     srt_stats S{};
     for (;;) {
         if (c->f->pending == 0) clear_host_flags(c, F);  // k_pass_end ORs into them
@@ -1748,6 +1989,20 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
         }
         c->f->dirty = true;
+        int mt_pos = 0;
+        if (use_mt) {
+            // this frame's stream starts where the previous frame's ended (device dump window) or at
+            // the caller's state
+            if (mt_chained) {
+                HIP_TRY(hipStreamWaitEvent(c->f->stream, c->mt_done, 0));
+                HIP_TRY(hipMemcpyAsync(mt_key0(c), mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToDevice, c->f->stream));
+                mt_pos = c->mt_pos;
+            } else {
+                if (c->mt_done) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->mt_done, 0));
+                HIP_TRY(hipMemcpyAsync(mt_key0(c), a->mt->key, rtmt::N * 4, hipMemcpyHostToDevice, c->f->stream));
+                mt_pos = a->mt->pos;
+            }
+        }
         for (int p = 0; p < F.npass; ++p) {
             const int s0 = p * batch;
             const int ns = std::min(batch, a->spp - s0);
@@ -1773,7 +2028,19 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.rows = c->rows;
             P.sample_base = a->sample_base + s0;
             P.spp = ns;
-            if (a->jitter) {
+            P.jit_plane = npix;
+            if (use_mt) {
+                // the pass's samples of the whole frame's stream (then the sizing draw after the last
+                // pass); a shard reads its rows by global pixel
+                const int64_t n_out = (int64_t)ns * 4 * W * Hf;
+                const int64_t n_skip = (p + 1 == F.npass) ? 4 * W * Hf : 0;
+                if (p > 0)
+                    HIP_TRY(hipMemcpyAsync(mt_key0(c), mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToDevice, c->f->stream));
+                if ((rc = mt_launch(c, c->f->stream, mt_pos, n_out, n_skip, c->f->jit, &mt_pos))) return rc;
+                P.jitter = c->f->jit;
+                P.jit_plane = W * Hf;
+                P.jit_global = 1;
+            } else if (a->jitter) {
                 const double* src = a->jitter + (int64_t)s0 * 4 * npix;
                 if (jit_dev) {
                     P.jitter = src;
@@ -1842,6 +2109,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->f->hit, (size_t)nrays * 4,
                                        hipMemcpyDeviceToHost, c->f->stream));
         }
+        if (use_mt) {
+            HIP_TRY(hipEventRecord(c->mt_done, c->f->stream));
+            c->mt_pos = mt_pos;
+        }
         uint32_t* hshadow = c->f->host + F.npass * F.pass_words;
         // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
         const bool fused = F.frame && F.npass == 1;
@@ -1851,9 +2122,36 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
         c->f->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
+        // the shard's tiles to rank 0 (RCCL over xGMI), assembled into the frame there
+        FrameSlot::Gather& G = c->f->gather;
+        G = FrameSlot::Gather{};
+        if (sharded) {
+            G.on = true;
+            G.W = W;
+            G.H = Hf;
+            G.npix = npix;
+            G.maxpix = maxpix;
+            G.want_u8 = true;
+            G.want_rgb = gather_rgb;
+            if (c->rank == 0) {
+                G.dst_u8 = (a->out_srgb8 && u8_dev) ? a->out_srgb8 : c->f->full_u8;
+                G.dst_rgb = (a->out_rgb && rgb_dev) ? a->out_rgb : c->f->full_rgb;
+                G.host_u8 = (a->out_srgb8 && !u8_dev) ? a->out_srgb8 : nullptr;
+                G.host_rgb = (a->out_rgb && !rgb_dev && gather_rgb) ? a->out_rgb : nullptr;
+            }
+        }
         if (async) {
-            // stats of this frame (and its errors) come with srt_render_finish; the next
-            // asynchronous frame goes to the other slot
+            // (a synchronous frame gathers after its retries: every rank gathers each frame once)
+            if (sharded && !c->defer_gather && (rc = gather_frame(c))) return rc;
+            // host outputs (pinned) are copied on the frame's stream; stats and errors come with
+            // srt_render_finish; the next asynchronous frame goes to the next slot
+            if (!sharded) {
+                if (a->out_rgb && !rgb_dev)
+                    HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->f->stream));
+                if (a->out_srgb8 && !u8_dev)
+                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->f->stream));
+            }
+            if (use_mt) c->mt_chain = a->mt;
             c->async_pending++;
             c->f->pending++;
             c->f->plan = F;
@@ -1861,9 +2159,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             c->next_slot = (c->last_slot + 1) % FRAME_SLOTS;
             return SRT_OK;
         }
-        if (a->out_rgb && !rgb_dev)
+        if (!sharded && a->out_rgb && !rgb_dev)
             HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->f->stream));
-        if (a->out_srgb8 && !u8_dev)
+        if (!sharded && a->out_srgb8 && !u8_dev)
             HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->f->stream));
         c->f->dirty = true;
         HIP_TRY(hipStreamSynchronize(c->f->stream));
@@ -1885,6 +2183,14 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         S.retries = retries;
         if (rc) return rc;
         break;
+    }
+    if (sharded && !c->defer_gather) {
+        if ((rc = gather_frame(c))) return rc;
+        HIP_TRY(hipStreamSynchronize(c->f->stream));
+    }
+    if (use_mt) {  // numpy's state after this frame's draws
+        HIP_TRY(hipMemcpy(a->mt->key, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost));
+        a->mt->pos = c->mt_pos;
     }
     if (st) {
         S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
@@ -2102,42 +2408,166 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
         return SRT_OK;
     }
     HIP_TRY(hipSetDevice(c->device));
-    constexpr int64_t NTAB = 31 * rtmt::N;
-    if (!c->mt) {
-        HIP_TRY(dalloc(&c->mt, NTAB + 3 * rtmt::N));
-        HIP_TRY(hipMemcpyAsync(c->mt, rtmt::tables_flat(), NTAB * 4, hipMemcpyHostToDevice, c->f->stream));
-    }
-    uint32_t* keys[2] = {c->mt + NTAB, c->mt + NTAB + rtmt::N};
-    uint32_t* dump = c->mt + NTAB + 2 * rtmt::N;
+    int rc = finish_async(c, nullptr);  // frames in flight may use the generator's scratch
+    if (rc) return rc;
+    if ((rc = mt_ensure(c))) return rc;
     double* dst = out;
     const bool host_out = n_out > 0 && !is_device_ptr(out);
     if (host_out) {
-        int rc = ensure_buf(&c->mt_out, c->mt_out_cap, n_out);
-        if (rc) return rc;
+        if ((rc = ensure_buf(&c->mt_out, c->mt_out_cap, n_out))) return rc;
         dst = c->mt_out;
     }
-    HIP_TRY(hipMemcpyAsync(keys[0], key, rtmt::N * 4, hipMemcpyHostToDevice, c->f->stream));
-    const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
-    for (size_t r = 0; r < plan.rounds.size(); ++r) {
-        const rtmt::Round& R = plan.rounds[r];
-        MtArgs A{};
-        A.key = keys[r & 1];
-        A.tab = c->mt;
-        A.out = dst;
-        A.chain_dst = R.chain ? keys[(r + 1) & 1] : nullptr;
-        A.dump_dst = R.dump_at >= 0 ? dump : nullptr;
-        A.words = R.words;
-        A.double_base = R.double_base;
-        A.n_out = n_out;
-        A.dump_at = R.dump_at;
-        A.pos = R.pos;
-        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), 0, c->f->stream, A);
-        HIP_TRY(hipGetLastError());
+    hipStream_t st = c->f->stream;
+    HIP_TRY(hipMemcpyAsync(mt_key0(c), key, rtmt::N * 4, hipMemcpyHostToDevice, st));
+    int final_pos = 0;
+    if ((rc = mt_launch(c, st, pos, n_out, n_skip, dst, &final_pos))) return rc;
+    if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(key_out, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *pos_out = final_pos;
+    return SRT_OK;
+}
+
+// ---- multi-GPU ------------------------------------------------------------------------------
+int srt_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(SRT_ERR_ARG, "null id");
+    static_assert(sizeof(ncclUniqueId) == SRT_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    memcpy(id, &u, sizeof(u));
+    return SRT_OK;
+}
+
+int srt_comm_init(srt_ctx* c, int nranks, int rank, const uint8_t* id) {
+    if (!c || !id || nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks)
+        return fail(SRT_ERR_ARG, "bad communicator arguments");
+    if (c->comm) return fail(SRT_ERR_ARG, "context already has a communicator");
+    HIP_TRY(hipSetDevice(c->device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    NCCL_TRY(ncclCommInitRank(&c->comm, nranks, u, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return SRT_OK;
+}
+
+int srt_comm_init_all(int ndev, const int* devs, srt_ctx** ctxs) {
+    if (ndev < 1 || ndev > MAX_RANKS || !devs || !ctxs) return fail(SRT_ERR_ARG, "bad device list");
+    for (int q = 0; q < ndev; ++q) ctxs[q] = nullptr;
+    for (int q = 0; q < ndev; ++q) {
+        int rc = srt_create(devs[q], &ctxs[q]);
+        if (rc) {
+            for (int k = 0; k < q; ++k) srt_destroy(ctxs[k]);
+            return rc;
+        }
     }
-    if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, c->f->stream));
-    HIP_TRY(hipMemcpyAsync(key_out, dump, rtmt::N * 4, hipMemcpyDeviceToHost, c->f->stream));
-    HIP_TRY(hipStreamSynchronize(c->f->stream));
-    *pos_out = plan.final_pos;
+    std::vector<ncclComm_t> comms(ndev);
+    ncclResult_t r = ncclCommInitAll(comms.data(), ndev, devs);
+    if (r != ncclSuccess) {
+        for (int k = 0; k < ndev; ++k) srt_destroy(ctxs[k]);
+        return fail(SRT_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    }
+    for (int q = 0; q < ndev; ++q) {
+        ctxs[q]->comm = comms[q];
+        ctxs[q]->nranks = ndev;
+        ctxs[q]->rank = q;
+    }
+    return SRT_OK;
+}
+
+int srt_comm_rank(srt_ctx* c, int* nranks, int* rank) {
+    if (!c || !nranks || !rank) return fail(SRT_ERR_ARG, "null argument");
+    *nranks = c->nranks;
+    *rank = c->rank;
+    return SRT_OK;
+}
+
+int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
+    if (!ctxs || n < 1 || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
+    for (int q = 0; q < n; ++q)
+        if (!ctxs[q] || ctxs[q]->nranks != n || ctxs[q]->rank != q)
+            return fail(SRT_ERR_ARG, "contexts must be the ranks 0..n-1 of one srt_comm_init_all group");
+    if (a->jitter) return fail(SRT_ERR_ARG, "a group frame draws its jitter on the devices (mt or Philox)");
+    if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
+    const bool want_rgb = a->out_rgb != nullptr;
+    int rc = SRT_OK;
+    srt_render_args aq = *a;
+    aq.flags = SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | (want_rgb ? SRT_RENDER_GATHER_RGB : 0);
+    aq.out_rgb = nullptr;  // rank 0 assembles into its slot buffers; copied to the caller's below
+    aq.out_srgb8 = nullptr;
+    for (int q = 0; q < n && !rc; ++q) {
+        if ((rc = finish_async(ctxs[q], nullptr))) break;
+        ctxs[q]->defer_gather = true;
+        rc = srt_render(ctxs[q], cam, &aq, nullptr);
+    }
+    FrameSlot* f0 = ctxs[0]->f;
+    if (!rc && n > 1) {
+        ncclResult_t r = ncclGroupStart();
+        for (int q = 0; q < n && !rc && r == ncclSuccess; ++q) {
+            (void)hipSetDevice(ctxs[q]->device);
+            rc = gather_post(ctxs[q]);
+        }
+        ncclResult_t r2 = ncclGroupEnd();
+        if (!rc && (r != ncclSuccess || r2 != ncclSuccess))
+            rc = fail(SRT_ERR_HIP, std::string("RCCL group gather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    }
+    if (!rc) {
+        (void)hipSetDevice(ctxs[0]->device);
+        rc = gather_finish(ctxs[0]);
+    }
+    srt_stats sum{};
+    for (int q = 0; q < n; ++q) {
+        ctxs[q]->defer_gather = false;
+        srt_stats sq{};
+        int r = srt_render_finish(ctxs[q], &sq);
+        if (!rc) rc = r;
+        if (q == 0) sum = sq;
+        else {
+            for (int d = 0; d < SRT_MAX_DEPTHS; ++d) sum.rays_per_depth[d] += sq.rays_per_depth[d];
+            sum.total_rays += sq.total_rays;
+            sum.shadow_rays += sq.shadow_rays;
+            sum.n_depths = std::max(sum.n_depths, sq.n_depths);
+        }
+    }
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(ctxs[0]->device));
+    const int64_t np = (int64_t)cam->width * cam->height;
+    if (a->out_srgb8) HIP_TRY(hipMemcpy(a->out_srgb8, f0->full_u8, (size_t)3 * np, hipMemcpyDefault));
+    if (want_rgb) HIP_TRY(hipMemcpy(a->out_rgb, f0->full_rgb, (size_t)3 * np * 8, hipMemcpyDefault));
+    if (st) *st = sum;
+    return SRT_OK;
+}
+
+int srt_comm_allreduce(srt_ctx* c, double* vals, int n, int op) {
+    if (!c || !vals || n < 1 || n > 64 || op < 0 || op > 1) return fail(SRT_ERR_ARG, "bad allreduce arguments");
+    if (c->nranks == 1 || !c->comm) return SRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = finish_async(c, nullptr);
+    if (rc) return rc;
+    if (!c->red) HIP_TRY(dalloc(&c->red, 64));
+    hipStream_t st = c->f->stream;
+    HIP_TRY(hipMemcpyAsync(c->red, vals, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    NCCL_TRY(ncclAllReduce(c->red, c->red, (size_t)n, ncclFloat64, op == 0 ? ncclSum : ncclMax, c->comm, st));
+    HIP_TRY(hipMemcpyAsync(vals, c->red, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SRT_OK;
+}
+
+int srt_comm_barrier(srt_ctx* c) {
+    double v = 0.0;
+    return srt_comm_allreduce(c, &v, 1, 0);
+}
+
+int srt_host_alloc(srt_ctx* c, int64_t bytes, void** out) {
+    if (!c || !out || bytes <= 0) return fail(SRT_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    return SRT_OK;
+}
+
+int srt_host_free(srt_ctx* c, void* p) {
+    if (!c) return fail(SRT_ERR_ARG, "null ctx");
+    if (p) HIP_TRY(hipHostFree(p));
     return SRT_OK;
 }
 

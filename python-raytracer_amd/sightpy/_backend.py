@@ -13,7 +13,7 @@ from . import _native as N
 from ._lower import lower_scene, camera_desc, collider_record
 from .utils.vector3 import vec3
 
-_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": None, "buffers": {}}
+_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": {}, "buffers": {}, "group": None}
 
 
 class RenderResult:
@@ -51,15 +51,47 @@ def context():
     return _STATE["lib"], _STATE["ctx"]
 
 
-def upload(scene, extra_media=(), force=False):
-    """Lower and upload `scene` unless the identical tables are already resident."""
-    lib, ctx = context()
+def devices():
+    """GPUs Scene.render uses: $SIGHTPY_DEVICES ("0,1,2,3" or "all"), else the one context device
+    ($SIGHTPY_DEVICE, else $LOCAL_RANK, else 0)."""
+    spec = os.environ.get("SIGHTPY_DEVICES", "").strip()
+    if not spec:
+        return [int(os.environ.get("SIGHTPY_DEVICE", os.environ.get("LOCAL_RANK", "0")))]
+    if spec == "all":
+        n = ctypes.c_int(0)
+        N.check(library(), library().srt_device_count(ctypes.byref(n)))
+        return list(range(n.value))
+    return [int(v) for v in spec.split(",") if v.strip()]
+
+
+def group():
+    """Contexts of the multi-GPU group over devices() (srt_comm_init_all: one RCCL communicator in
+    this process, rank q on devices()[q]), created once."""
+    devs = devices()
+    g = _STATE["group"]
+    if g is not None and g[0] == devs:
+        return library(), g[1]
+    lib = library()
+    arr = (ctypes.c_int * len(devs))(*devs)
+    ctxs = (ctypes.c_void_p * len(devs))()
+    N.check(lib, lib.srt_comm_init_all(len(devs), arr, ctxs))
+    _STATE["group"] = (devs, ctxs)
+    return lib, ctxs
+
+
+def upload(scene, extra_media=(), force=False, ctx=None):
+    """Lower and upload `scene` to `ctx` (default: the process context) unless the identical tables
+    are already resident there."""
+    lib = library()
+    if ctx is None:
+        ctx = context()[1]
     L = lower_scene(scene, extra_media)
     sig = L.signature()
-    if force or sig != _STATE["scene_sig"]:
-        _STATE["scene_sig"] = None
+    key = ctx.value if isinstance(ctx, ctypes.c_void_p) else int(ctx)
+    if force or sig != _STATE["scene_sig"].get(key):
+        _STATE["scene_sig"].pop(key, None)
         N.check(lib, lib.srt_upload_scene(ctx, ctypes.byref(L.desc())))
-        _STATE["scene_sig"] = sig
+        _STATE["scene_sig"][key] = sig
     return L
 
 
@@ -78,6 +110,14 @@ def device_buffer(name, nbytes):
     return p
 
 
+def release_buffer(name):
+    """Free a named device allocation of the context."""
+    cur = _STATE["buffers"].pop(name, None)
+    if cur is not None:
+        lib, ctx = context()
+        N.check(lib, lib.srt_device_free(ctx, cur[0]))
+
+
 def numpy_uniforms(n_out, n_skip=0, out=None):
     """`np.random.rand(n_out)` computed on the GPU (then `n_skip` more draws), advancing numpy's
     global RandomState exactly as the host draws would (srt_mt19937_uniforms).
@@ -89,6 +129,8 @@ def numpy_uniforms(n_out, n_skip=0, out=None):
     if name != "MT19937":
         raise ValueError("numpy's global generator is not MT19937")
     key = np.ascontiguousarray(key, dtype=np.uint32)
+    if out is None:
+        release_buffer("uniforms")  # sized per call, not kept at the largest request ever made
     dst = device_buffer("uniforms", 8 * n_out) if out is None else N.ptr(out)
     key_out = np.empty(624, dtype=np.uint32)
     pos_out = ctypes.c_int32(0)
@@ -114,9 +156,11 @@ def _default_seed():
 
 
 def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False,
-                 jitter_device=None):
+                 jitter_device=None, mt=False):
     """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG;
-    `jitter_device`: the same uniforms already in device memory (numpy_uniforms)."""
+    `jitter_device`: the same uniforms already in device memory (numpy_uniforms); `mt=True`: the
+    jitter is numpy's global stream generated on the device (the reference's draws, including the
+    sizing draw of scene.py:81), and numpy's global state is advanced past it."""
     lib, ctx = context()
     upload(scene)
     cam = scene.camera
@@ -140,6 +184,12 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
             raise ValueError("jitter must have shape (spp, 4, %d)" % npix)
         a.jitter = N.ptr(j)
     a.seed = int(seed if seed is not None else _default_seed()) & (2**64 - 1)
+    state = None
+    if mt:
+        if j is not None or jitter_device is not None:
+            raise ValueError("mt=True draws the jitter itself")
+        state = N.MtState.from_numpy()
+        a.mt = ctypes.pointer(state)
     rgb = np.empty((3, npix)) if want_rgb else None
     u8 = np.empty((npix, 3), dtype=np.uint8)
     hits = np.empty((spp, npix), dtype=np.int32) if want_hits else None
@@ -148,7 +198,36 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
     a.out_hit_id = N.ptr(hits)
     st = N.Stats()
     N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
+    if state is not None:
+        state.to_numpy()
     return RenderResult(u8.reshape(nrows, W, 3), rgb, hits, st.as_dict())
+
+
+def render_group(scene, spp, seed=None, batch_size=None, want_rgb=True, mt=True):
+    """Scene.render on every GPU of devices(): each renders its 8-row bands (SRT_RENDER_SHARDED) and
+    the tiles are gathered to the first over RCCL (srt_render_group).  `mt`: numpy's stream as in
+    render_scene (else the device RNG)."""
+    lib, ctxs = group()
+    for q in range(len(ctxs)):
+        upload(scene, ctx=ctypes.c_void_p(ctxs[q]))
+    cam = scene.camera
+    W, H = int(cam.screen_width), int(cam.screen_height)
+    cd = camera_desc(cam)
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = int(spp), 0, H, int(batch_size or 0)
+    a.seed = int(seed if seed is not None else _default_seed()) & (2**64 - 1)
+    state = None
+    if mt:
+        state = N.MtState.from_numpy()
+        a.mt = ctypes.pointer(state)
+    rgb = np.empty((3, W * H)) if want_rgb else None
+    u8 = np.empty((W * H, 3), dtype=np.uint8)
+    a.out_rgb, a.out_srgb8 = N.ptr(rgb), N.ptr(u8)
+    st = N.Stats()
+    N.check(lib, lib.srt_render_group(ctxs, len(ctxs), ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
+    if state is not None:
+        state.to_numpy()
+    return RenderResult(u8.reshape(H, W, 3), rgb, None, st.as_dict())
 
 
 def _media_of(ray_n, count):

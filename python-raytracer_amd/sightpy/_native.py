@@ -122,6 +122,25 @@ class CameraDesc(ctypes.Structure):
     ]
 
 
+class MtState(ctypes.Structure):
+    """np.random.get_state() of numpy's legacy MT19937 RandomState (srt_mt_state)."""
+    _fields_ = [("key", ctypes.c_uint32 * 624), ("pos", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+    @classmethod
+    def from_numpy(cls, state=None):
+        name, key, pos, _, _ = np.random.get_state() if state is None else state
+        if name != "MT19937":
+            raise ValueError("numpy's global generator is not MT19937")
+        m = cls()
+        np.ctypeslib.as_array(m.key)[:] = np.asarray(key, dtype=np.uint32)
+        m.pos = int(pos)
+        return m
+
+    def to_numpy(self):
+        """Set numpy's global RandomState to this state (the gauss cache is reset, as rand leaves it)."""
+        np.random.set_state(("MT19937", np.ctypeslib.as_array(self.key).copy(), int(self.pos), 0, 0.0))
+
+
 class RenderArgs(ctypes.Structure):
     _fields_ = [
         ("spp", ctypes.c_int32),
@@ -130,6 +149,7 @@ class RenderArgs(ctypes.Structure):
         ("batch_spp", ctypes.c_int32),
         ("rows", _p),
         ("jitter", _p),
+        ("mt", ctypes.POINTER(MtState)),
         ("seed", ctypes.c_uint64),
         ("out_rgb", _p),
         ("out_srgb8", _p),
@@ -189,8 +209,9 @@ class TraceArgs(ctypes.Structure):
 
 
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
-RENDER_ASYNC = 1  # SRT_RENDER_ASYNC
-ABI_VERSION = 3  # SRT_ABI_VERSION of include/sightpy_rt.h
+RENDER_ASYNC, RENDER_SHARDED, RENDER_GATHER_RGB = 1, 2, 4  # SRT_RENDER_*
+ABI_VERSION = 4  # SRT_ABI_VERSION of include/sightpy_rt.h
+COMM_ID_BYTES = 128
 
 SIGNATURES = {
     "srt_abi_version": (ctypes.c_int, []),
@@ -212,6 +233,16 @@ SIGNATURES = {
     "srt_synchronize": (ctypes.c_int, [_p]),
     "srt_render_finish": (ctypes.c_int, [_p, ctypes.POINTER(Stats)]),
     "srt_stream": (ctypes.c_int, [_p, ctypes.POINTER(_p)]),
+    "srt_comm_unique_id": (ctypes.c_int, [_p]),
+    "srt_comm_init": (ctypes.c_int, [_p, ctypes.c_int, ctypes.c_int, _p]),
+    "srt_comm_init_all": (ctypes.c_int, [ctypes.c_int, _p, _p]),
+    "srt_comm_rank": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "srt_render_group": (ctypes.c_int, [_p, ctypes.c_int, ctypes.POINTER(CameraDesc), ctypes.POINTER(RenderArgs),
+                                        ctypes.POINTER(Stats)]),
+    "srt_comm_allreduce": (ctypes.c_int, [_p, _p, ctypes.c_int, ctypes.c_int]),
+    "srt_comm_barrier": (ctypes.c_int, [_p]),
+    "srt_host_alloc": (ctypes.c_int, [_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
+    "srt_host_free": (ctypes.c_int, [_p, _p]),
     "srt_last_error": (ctypes.c_char_p, []),
 }
 

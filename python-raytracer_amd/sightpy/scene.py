@@ -2,9 +2,9 @@
 
 `Scene` keeps the reference's assembly API.  `render()` is the drop-in boundary: instead of the
 reference's `multiprocessing.Pool` over samples (scene.py:80-116) it lowers the scene to flat
-device tables once, uploads the camera jitter drawn from numpy's global RNG in the reference's
-order (so a seeded render consumes the same random stream), and runs the whole
-samples x depths wavefront plus the sRGB resolve on the GPU through `libsightpy_hip.so`.
+device tables once, generates the camera jitter of numpy's global RNG in the reference's order on
+the GPU (so a seeded render consumes the same random stream), and runs the whole
+samples x depths wavefront plus the sRGB resolve on the GPU(s) through `libsightpy_hip.so`.
 """
 import time
 
@@ -62,48 +62,39 @@ class Scene:
 
         rng="numpy" (default) draws the primary-ray jitter from numpy's global legacy RNG exactly
         as the reference does (including the extra sizing draw at scene.py:81), so seeded renders
-        match the reference: the stream is generated on the GPU (srt_mt19937_uniforms, bit-equal to
-        np.random.rand) and numpy's global state is advanced past it.  rng="numpy-host" draws the
-        same stream with numpy on the host.  rng="device" generates independent jitter on the GPU
-        (Philox keyed by pixel and sample).  `batch_size` bounds the samples per device pass.
+        match the reference: the stream is generated on the GPU inside the render (rt_mt.h,
+        bit-equal to np.random.rand) and numpy's global state is advanced past it.
+        rng="numpy-host" draws the same stream with numpy on the host.  rng="device" generates
+        independent jitter on the GPU (Philox keyed by pixel and sample).  `batch_size` bounds the
+        samples per device pass.
+
+        With several GPUs ($SIGHTPY_DEVICES, e.g. "0,1,2,3" or "all") the frame is split into
+        8-row bands dealt round-robin over the GPUs and gathered over RCCL (the reference's
+        multiprocessing.Pool over samples, scene.py:80-116, is replaced); the image does not depend
+        on the number of GPUs.
         """
-        from ._backend import render_scene, numpy_uniforms
+        from . import _backend as B
 
         print("Rendering...")
         t0 = time.time()
-        world, rank = _dist_world()
-        jitter = jitter_dev = None
-        npix = int(self.camera.screen_width) * int(self.camera.screen_height)
-        if rng == "numpy" and world == 1:
-            jitter_dev = numpy_uniforms(samples_per_pixel * 4 * npix, 4 * npix)
-        elif rng in ("numpy", "numpy-host"):
-            jitter = self.camera.draw_jitter(samples_per_pixel)
-            self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
-        elif rng != "device":
+        if rng not in ("numpy", "numpy-host", "device"):
             raise ValueError("rng must be 'numpy', 'numpy-host' or 'device'")
-        if world == 1:
-            # only the uint8 image leaves the GPU (the linear RGB stays there: 8x fewer PCIe bytes)
-            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size,
-                               jitter_device=jitter_dev, want_rgb=False)
-            srgb8 = out.srgb8
+        H, W = int(self.camera.screen_height), int(self.camera.screen_width)
+        ndev = len(B.devices())
+        if ndev > 1 and rng != "numpy-host" and H >= 8 * ndev:
+            out = B.render_group(self, samples_per_pixel, seed=seed, batch_size=batch_size, want_rgb=False,
+                                 mt=(rng == "numpy"))
         else:
-            # one process per GPU under torch.distributed: render this rank's row bands, gather
-            import torch
-            from ._shard import shard_rows, gather_rows
-
-            H, W = int(self.camera.screen_height), int(self.camera.screen_width)
-            rows = shard_rows(H, world, rank)
-            if jitter is not None:
-                jitter = jitter.reshape(samples_per_pixel, 4, H, W)[:, :, rows].reshape(samples_per_pixel, 4, -1)
-            out = render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size, rows=rows,
-                               want_rgb=False)
-            tile = torch.from_numpy(out.srgb8)
-            if torch.distributed.get_backend() == "nccl":
-                tile = tile.cuda()
-            srgb8 = gather_rows(tile, H, world).cpu().numpy()
+            jitter = None
+            if rng == "numpy-host":
+                jitter = self.camera.draw_jitter(samples_per_pixel)
+                self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
+            # only the uint8 image leaves the GPU (the linear RGB stays there: 8x fewer PCIe bytes)
+            out = B.render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size,
+                                 want_rgb=False, mt=(rng == "numpy"))
         self.last_stats = out.stats
         print("Render Took", time.time() - t0)
-        return Image.fromarray(srgb8, "RGB")
+        return Image.fromarray(out.srgb8, "RGB")
 
     def get_distances(self):
         """Grey depth map of one primary sample (reference scene.py:142-166)."""
@@ -119,19 +110,6 @@ class Scene:
         h, w = self.camera.screen_height, self.camera.screen_width
         u8 = (255 * np.clip(g, 0, 1).reshape((h, w))).astype(np.uint8)
         return Image.fromarray(np.stack([u8, u8, u8], axis=-1), "RGB")
-
-
-def _dist_world():
-    """(world size, rank) of an initialised torch.distributed job, else (1, 0)."""
-    import sys
-
-    if "torch.distributed" not in sys.modules:
-        return 1, 0
-    import torch.distributed as dist
-
-    if not (dist.is_available() and dist.is_initialized()):
-        return 1, 0
-    return dist.get_world_size(), dist.get_rank()
 
 
 def get_raycolor_tuple(x):

@@ -73,9 +73,9 @@ PROBE = r"""
 #define O(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
   S(srt_collider) S(srt_material) S(srt_texture) S(srt_light) S(srt_scene_desc) S(srt_camera)
-  S(srt_render_args) S(srt_stats) S(srt_trace_args)
+  S(srt_render_args) S(srt_stats) S(srt_trace_args) S(srt_mt_state)
   O(srt_collider, p) O(srt_material, p) O(srt_texture, lut) O(srt_stats, total_rays)
-  O(srt_render_args, out_hit_id) O(srt_camera, xs)
+  O(srt_render_args, out_hit_id) O(srt_render_args, seed) O(srt_camera, xs)
   return 0;
 }
 """
@@ -103,4 +103,6 @@ def test_struct_layout_matches_binding(tmp_path):
         assert vals[name] == ctypes.sizeof(cls), name
     assert vals["srt_stats.total_rays"] == N.Stats.total_rays.offset
     assert vals["srt_render_args.out_hit_id"] == N.RenderArgs.out_hit_id.offset
+    assert vals["srt_render_args.seed"] == N.RenderArgs.seed.offset
+    assert vals["srt_mt_state"] == ctypes.sizeof(N.MtState)
     assert vals["srt_camera.xs"] == N.CameraDesc.xs.offset

@@ -1,7 +1,18 @@
-"""Multi-rank row sharding: world-size-2 `gloo` jobs on the CPU for the shard /
-gather / assembly logic and for `Scene.render` under torch.distributed (with the per-rank device
-render replaced by a stand-in that encodes which rows and jitter it was given), plus one GPU test in
-which two ranks share the card and their gathered image must equal the single-process render."""
+"""Multi-GPU row sharding.
+
+The product path is torch-free: the library splits a frame into 8-row bands dealt round-robin over
+the ranks (SRT_RENDER_SHARDED, rt_device.h shard_of_row / shard_local_row) and gathers the tiles
+to rank 0 over RCCL (rt_kernels.hip gather_post / k_assemble).  On the CPU:
+  * the kernels' shard map (compiled for the CPU) against the numpy restatement (sightpy._shard);
+  * a world-size-2 `gloo` job replays the gather protocol -- each rank sends its unpadded tile,
+    rank 0 receives into padded staging and assembles with the kernels' map -- and must rebuild
+    the frame exactly.
+On the GPU (one card): the sharded render through a 1-rank communicator (multi-process API) and a
+1-device srt_comm_init_all group (single-process API) equal the plain render, and every rank's
+shard of an N-rank frame, rendered in turn, assembles into the plain render (the numpy-stream
+jitter is indexed by global pixel).  The N > 1 RCCL exchange itself runs only on a multi-GPU node.
+"""
+import ctypes
 import os
 import socket
 import sys
@@ -9,7 +20,6 @@ from pathlib import Path
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 ROOT = Path(__file__).resolve().parent.parent
 
@@ -22,26 +32,7 @@ def _free_port():
     return port
 
 
-def _init(rank, world, port):
-    for p in (ROOT / "python-raytracer_amd", ROOT / "tests", ROOT / "oracle"):
-        sys.path.insert(0, str(p))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    import torch.distributed as dist
-
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    return dist
-
-
-def _spawn(fn, world, *args):
-    port = _free_port()
-    mp.start_processes(fn, args=(world, port) + args, nprocs=world, join=True, start_method="spawn")
-
-
-# ---------------------------------------------------------------------------------------------
-
-
 def test_shard_rows_partition():
-    sys.path.insert(0, str(ROOT / "python-raytracer_amd"))
     from sightpy._shard import shard_rows, assemble_index, max_shard_rows
 
     for H in (1, 7, 8, 37, 300, 1080):
@@ -49,9 +40,8 @@ def test_shard_rows_partition():
             parts = [shard_rows(H, world, r) for r in range(world)]
             allrows = np.sort(np.concatenate(parts))
             assert np.array_equal(allrows, np.arange(H))
-            assert max(len(p) for p in parts) == max_shard_rows(H, world)
+            assert max(len(p) for p in parts) == max_shard_rows(H, world) == len(parts[0])
             idx = assemble_index(H, world)
-            # gathered buffer of padded tiles -> image rows
             buf = np.full(world * max_shard_rows(H, world), -1)
             for r, p in enumerate(parts):
                 buf[r * max_shard_rows(H, world) + np.arange(len(p))] = p
@@ -60,90 +50,193 @@ def test_shard_rows_partition():
     assert [len(shard_rows(1080, 8, r)) for r in range(8)] == [136] * 7 + [128]
 
 
-def _gather_worker(rank, world, port, H, W):
-    dist = _init(rank, world, port)
-    import torch
-    from sightpy._shard import shard_rows, gather_rows
+def _kernel_shard_map(H, n):
+    import hostcheck as HC
 
+    owner = np.empty(H, dtype=np.int32)
+    local = np.empty(H, dtype=np.int64)
+    lib = HC.lib()
+    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.hc_shard_map(H, n, owner.ctypes.data, local.ctypes.data)
+    return owner, local
+
+
+@pytest.mark.parametrize("H", [8, 37, 300, 1080, 2160])
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
+def test_kernel_shard_map_matches_partition(H, n):
+    from sightpy._shard import shard_rows
+
+    owner, local = _kernel_shard_map(H, n)
+    for q in range(n):
+        rows = shard_rows(H, n, q)
+        assert np.array_equal(np.where(owner == q)[0], rows)
+        assert np.array_equal(local[rows], np.arange(len(rows)))
+
+
+def _gather_worker(rank, world, port, H, W):
+    for p in (ROOT / "python-raytracer_amd", ROOT / "tests", ROOT / "oracle"):
+        sys.path.insert(0, str(p))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from sightpy._shard import shard_rows
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     full = np.random.default_rng(7).integers(0, 256, size=(H, W, 3), dtype=np.uint8)
+    rgb = np.random.default_rng(8).random((3, H * W))
     rows = shard_rows(H, world, rank)
-    out = gather_rows(torch.from_numpy(full[rows].copy()), H, world).numpy()
-    assert np.array_equal(out, full), rank
+    tile_u8 = full[rows].copy()
+    tile_rgb = rgb.reshape(3, H, W)[:, rows].reshape(3, -1).copy()
+    if rank == 0:
+        maxpix = len(shard_rows(H, world, 0)) * W
+        g_u8 = np.zeros((world, maxpix * 3), dtype=np.uint8)
+        g_rgb = np.zeros((world, 3 * maxpix))
+        g_u8[0, : tile_u8.size] = tile_u8.reshape(-1)
+        g_rgb[0, : tile_rgb.size] = tile_rgb.reshape(-1)
+        for q in range(1, world):
+            npq = len(shard_rows(H, world, q)) * W
+            bu = torch.zeros(3 * npq, dtype=torch.uint8)
+            br = torch.zeros(3 * npq, dtype=torch.float64)
+            dist.recv(bu, q)
+            dist.recv(br, q)
+            g_u8[q, : 3 * npq] = bu.numpy()
+            g_rgb[q, : 3 * npq] = br.numpy()
+        # k_assemble with the kernels' map
+        owner, local = _kernel_shard_map(H, world)
+        out_u8 = np.empty((H, W, 3), dtype=np.uint8)
+        out_rgb = np.empty((3, H, W))
+        for y in range(H):
+            q, i = owner[y], local[y]
+            npq = len(shard_rows(H, world, q)) * W
+            out_u8[y] = g_u8[q, 3 * i * W: 3 * (i + 1) * W].reshape(W, 3)
+            for ch in range(3):
+                out_rgb[ch, y] = g_rgb[q, ch * npq + i * W: ch * npq + (i + 1) * W]
+        assert np.array_equal(out_u8, full)
+        assert np.array_equal(out_rgb.reshape(3, -1), rgb)
+    else:
+        dist.send(torch.from_numpy(tile_u8.reshape(-1)), 0)
+        dist.send(torch.from_numpy(tile_rgb.reshape(-1)), 0)
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("H", [37, 48])
-def test_gather_rows_gloo_world2(H):
-    _spawn(_gather_worker, 2, H, 5)
+def test_gather_protocol_gloo_world2(H):
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_gather_worker, args=(2, _free_port(), H, 5), nprocs=2, join=True, start_method="spawn")
 
 
-def _render_worker(rank, world, port):
-    dist = _init(rank, world, port)
-    import scenes
-    from sightpy import _backend
-
-    W, H, spp = 16, 20, 2
-    calls = []
-
-    def fake_render_scene(scene, spp_, jitter=None, seed=None, batch_size=None, rows=None, **kw):
-        # stand-in for the device: pixel = (row, column, first jitter draw) so the test can check
-        # which rows and which slice of the numpy jitter stream this rank rendered
-        calls.append(rows)
-        n = len(rows)
-        j = jitter.reshape(spp_, 4, n, W)
-        u8 = np.zeros((n, W, 3), dtype=np.uint8)
-        u8[..., 0] = np.asarray(rows)[:, None]
-        u8[..., 1] = np.arange(W)[None, :]
-        u8[..., 2] = (j[0, 0] * 255).astype(np.uint8)
-        return _backend.RenderResult(u8, None, None, {"total_rays": n * W * spp_})
-
-    _backend.render_scene = fake_render_scene
-    sc = scenes.example1(W, H)
-    np.random.seed(3)
-    img = np.asarray(sc.render(spp))
-    np.random.seed(3)
-    jit = np.random.rand(spp * 4 * H * W).reshape(spp, 4, H, W)
-    assert img.shape == (H, W, 3)
-    assert np.array_equal(img[..., 0], np.repeat(np.arange(H)[:, None], W, 1))
-    assert np.array_equal(img[..., 1], np.repeat(np.arange(W)[None, :], H, 0))
-    assert np.array_equal(img[..., 2], (jit[0, 0] * 255).astype(np.uint8))
-    assert len(calls) == 1 and len(calls[0]) < H
-    dist.barrier()
-    dist.destroy_process_group()
+# ---- GPU ------------------------------------------------------------------------------------
 
 
-def test_scene_render_distributed_gloo_world2():
-    _spawn(_render_worker, 2)
-
-
-# ---------------------------------------------------------------------------------------------
-
-
-def _gpu_worker(rank, world, port, out_path):
-    dist = _init(rank, world, port)
-    import scenes
-
-    os.environ["SIGHTPY_DEVICE"] = "0"  # both ranks share the one card of the test box
-    sc = scenes.example1(96, 40, 3)
-    np.random.seed(11)
-    img = np.asarray(sc.render(2))
-    if rank == 0:
-        np.save(out_path, img)
-    dist.barrier()
-    dist.destroy_process_group()
+def _render_args(N, spp, H, flags, mt=None, u8=None, rgb=None, seed=5):
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, H, 0
+    a.mt = ctypes.pointer(mt) if mt is not None else None
+    a.seed = seed
+    a.flags = flags
+    a.out_srgb8 = N.ptr(u8)
+    a.out_rgb = N.ptr(rgb)
+    return a
 
 
 @pytest.mark.gpu
-def test_scene_render_two_ranks_equals_single_gpu(tmp_path):
+def test_gpu_sharded_frame_one_rank_communicator_equals_plain_render():
+    """SRT_RENDER_SHARDED through a 1-rank RCCL communicator (srt_comm_unique_id / srt_comm_init, the
+    multi-process API bench.py uses), synchronous and pipelined, equals the plain render."""
     import scenes
+    from sightpy import _backend as B, _native as N
 
-    out = tmp_path / "two.npy"
-    _spawn(_gpu_worker, 2, str(out))
     sc = scenes.example1(96, 40, 3)
     np.random.seed(11)
-    ref = np.asarray(sc.render(2))
-    # framebuffer atomics at depth >= 1 add in a run-dependent order (f64 rounding), so a u8 value
-    # may differ by one at a rounding boundary
-    d = np.abs(np.load(out).astype(int) - ref.astype(int))
-    assert d.max() <= 1 and (d > 0).mean() < 1e-3
+    ref = B.render_scene(sc, 2, seed=5, mt=True)
+    after_ref = np.random.get_state()[1].copy()
+    lib = B.library()
+    ctx = ctypes.c_void_p()
+    N.check(lib, lib.srt_create(int(B.devices()[0]), ctypes.byref(ctx)))
+    try:
+        cid = (ctypes.c_uint8 * N.COMM_ID_BYTES)()
+        N.check(lib, lib.srt_comm_unique_id(cid))
+        N.check(lib, lib.srt_comm_init(ctx, 1, 0, cid))
+        B.upload(sc, ctx=ctx)
+        cd = B.camera_desc(sc.camera)
+        np.random.seed(11)
+        mt = N.MtState.from_numpy()
+        u8 = np.empty((40 * 96, 3), np.uint8)
+        rgb = np.empty((3, 40 * 96))
+        a = _render_args(N, 2, 40, N.RENDER_SHARDED | N.RENDER_GATHER_RGB, mt, u8, rgb)
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+        np.testing.assert_allclose(rgb, ref.rgb, rtol=1e-12, atol=1e-15)
+        assert np.array_equal(u8.reshape(40, 96, 3), ref.srgb8)
+        assert np.array_equal(np.ctypeslib.as_array(mt.key), after_ref)
+        # four pipelined frames into pinned host buffers, the stream continuing on the device
+        bufs = []
+        for _ in range(4):
+            pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * 40 * 96, ctypes.byref(pu)))
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * 40 * 96 * 8, ctypes.byref(pr)))
+            bufs.append((pu, pr))
+        np.random.seed(11)
+        mt2 = N.MtState.from_numpy()
+        a2 = _render_args(N, 2, 40, N.RENDER_SHARDED | N.RENDER_GATHER_RGB | N.RENDER_ASYNC, mt2)
+        for pu, pr in bufs:
+            a2.out_srgb8, a2.out_rgb = pu, pr
+            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a2), None))
+        N.check(lib, lib.srt_render_finish(ctx, None))
+        np.random.seed(11)
+        for pu, pr in bufs:
+            want = B.render_scene(sc, 2, seed=5, mt=True)
+            got = np.ctypeslib.as_array(ctypes.cast(pr, ctypes.POINTER(ctypes.c_double)), shape=(3, 40 * 96))
+            np.testing.assert_allclose(got, want.rgb, rtol=1e-12, atol=1e-15)
+            got8 = np.ctypeslib.as_array(ctypes.cast(pu, ctypes.POINTER(ctypes.c_uint8)), shape=(40 * 96 * 3,))
+            assert np.array_equal(got8.reshape(40, 96, 3), want.srgb8)
+        assert np.array_equal(np.ctypeslib.as_array(mt2.key), np.random.get_state()[1])
+        assert mt2.pos == np.random.get_state()[2]
+        for pu, pr in bufs:
+            lib.srt_host_free(ctx, pu)
+            lib.srt_host_free(ctx, pr)
+    finally:
+        lib.srt_destroy(ctx)
+
+
+@pytest.mark.gpu
+def test_gpu_group_render_one_device_equals_plain_render(monkeypatch):
+    """srt_comm_init_all + srt_render_group (the single-process multi-GPU API Scene.render uses with
+    $SIGHTPY_DEVICES) on a group of one device."""
+    import scenes
+    from sightpy import _backend as B
+
+    monkeypatch.setenv("SIGHTPY_DEVICES", str(B.devices()[0]))
+    sc = scenes.example3(64, 48, 6)
+    np.random.seed(4)
+    ref = B.render_scene(sc, 2, seed=5, mt=True)
+    np.random.seed(4)
+    got = B.render_group(sc, 2, seed=5, mt=True)
+    np.testing.assert_allclose(got.rgb, ref.rgb, rtol=1e-12, atol=1e-15)
+    assert np.array_equal(got.srgb8, ref.srgb8)
+    assert got.stats["total_rays"] == ref.stats["total_rays"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gpu_every_shard_of_an_n_rank_frame_assembles_to_the_plain_render(world):
+    """What each rank of an N-rank job renders (its 8-row bands, jitter read from the whole frame's
+    numpy stream by global pixel), rendered here one shard after another on one card and assembled
+    with the partition, equals the single-GPU frame; numpy's state advances identically."""
+    import scenes
+    from sightpy import _backend as B
+    from sightpy._shard import shard_rows
+
+    sc = scenes.example1(120, 64, 4)
+    np.random.seed(21)
+    full = B.render_scene(sc, 3, seed=5, mt=True)
+    after = np.random.get_state()[1].copy()
+    rgb = np.zeros((3, 64, 120))
+    for q in range(world):
+        rows = shard_rows(64, world, q)
+        np.random.seed(21)
+        part = B.render_scene(sc, 3, seed=5, mt=True, rows=rows)
+        assert np.array_equal(np.random.get_state()[1], after)
+        rgb[:, rows] = part.rgb.reshape(3, len(rows), 120)
+    np.testing.assert_allclose(rgb.reshape(3, -1), full.rgb, rtol=1e-12, atol=1e-15)

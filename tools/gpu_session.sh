@@ -23,23 +23,18 @@ for step in "$@"; do
     tests) run tests 900 python3 -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
-    bench_sync) run bench_sync 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sync ;;
-    prof_sync) run prof_sync 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sync -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sync ;;
+    shard8) for n in 2 4 8; do run "bench_shard$n" 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of $n; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
     configs) for c in example3_1080p_d8 example4_4k_d6 cornell_800_s512; do run "bench_$c" 600 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline; done ;;
-    occ) for o in 0 2 3 4; do run "bench_occ$o" 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --occupancy $o; done ;;
-    abl) for f in build/abl/libsightpy_hip_*.so; do n=$(basename $f .so); run "abl_${n#libsightpy_hip_}" 300 env SIGHTPY_HIP_LIB=$f python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline; done ;;
     pmc_list) run pmc_list 120 rocprofv3 -L ;;
     pmc_sq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_sq1 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
             run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    shard8) run bench_shard8 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 8
-            run bench_shard4 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 4
-            run bench_shard2 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of 2 ;;
-    latency) run prof_latency 300 rocprofv3 --kernel-trace -d gpurun_out/prof_latency -o lat --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --size 64x1 --spp 1
-             run prof_shard8 300 rocprofv3 --kernel-trace -d gpurun_out/prof_shard8 -o s8 --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --shard-of 8 ;;
-    rehearse) run rehearse_gloo2 300 env SIGHTPY_BENCH_DEVICE=0 SIGHTPY_BENCH_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 1 ;;
+    mctests) run mctests 600 python3 -u -m pytest tests/test_gpu_mc.py -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
+    mt) run mt 300 python3 tools/mt_timing.py ;;
+    api) run api 300 python3 tools/api_timing.py --repeats 5 --profile ;;
+    api_prof) run api_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/api_prof -o api --output-format csv -- python3 tools/api_timing.py --repeats 5 ;;
     rngdev) run bench_rngdev 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --rng device ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
