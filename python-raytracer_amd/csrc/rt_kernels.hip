@@ -895,7 +895,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, cons
 // ---- numpy legacy RNG stream on the device (rt_mt.h) ---------------------------------------------
 struct MtArgs {
     const uint32_t* key;   // the round's key window (624 words)
-    const uint32_t* tab;   // jump tables: J1[16][624] then J2[15][624]
+    const uint32_t* tab;   // jump polynomials x^(sL-1), s = 1..SEGS-1 (624 words each)
     double* out;           // doubles of the whole call
     uint32_t* chain_dst;   // next round's key window (written by segment SEGS-1) or null
     uint32_t* dump_dst;    // final numpy key window or null
@@ -903,13 +903,26 @@ struct MtArgs {
     int64_t double_base;   // first double of this round
     int64_t n_out;         // doubles to write (the rest are skipped draws)
     int64_t dump_at;       // round-relative start of the final state window, or -1
+    int64_t plane;         // doubles per jitter plane (0: write every double)
+    int32_t plane_mask;    // bit k set: write the doubles of planes with index % 4 == k
     int32_t pos;           // outputs start at word `pos` of the key window
 };
 
-constexpr int MT_THREADS = 320;  // 5 waves: one output pair per thread per 624-word block
-// LDS ring of 624-word blocks: block q in slot q % 3, slot 3 mirrors slot 0 so that any two
-// consecutive blocks are contiguous (slots s, s + 1)
-constexpr int MT_SLOTS = 4;
+// One workgroup per segment.  Jump: y = the 34 x 624 raw words generated from the key window (LDS),
+// then W'[m] = XOR_{i : p_i} y[i + m] -- wave v takes coefficient words [78 v, 78 v + 78), lane g the
+// ten outputs m = 10 g .. 10 g + 9 with y[32 w + 10 g .. + 41] in registers, so a set bit costs ten
+// register XORs and no LDS traffic; the eight waves' partial windows are XOR-reduced through LDS.
+// Generation: a ring of three 624-word blocks; threads < 227 make the next block (three dependent
+// words each) while threads < 312 temper and store the current block's 312 doubles.
+constexpr int MT_THREADS = 512;
+constexpr int MT_WAVES = MT_THREADS / 64;
+constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 78 coefficient words
+constexpr int MT_G = 10;                              // window outputs per lane in the jump
+constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
+constexpr int MT_RED = 640;                           // per-wave stride of the reduction buffer
+static_assert(MT_CW_PER_WAVE * MT_WAVES == rtmt::N, "coefficient words split evenly over the waves");
+static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 42 <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
+static_assert(3 * rtmt::N + MT_WAVES * MT_RED <= MT_YBLOCKS * rtmt::N, "ring and reduction alias y");
 
 // workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic, not for its global
 // stores (__syncthreads() would also drain the output stores every block)
@@ -918,138 +931,139 @@ __device__ __forceinline__ void mt_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-__device__ __forceinline__ void mt_store(uint32_t* ring, int slot, int i, uint32_t v) {
-    ring[slot * rtmt::N + i] = v;
-    if (slot == 0) ring[3 * rtmt::N + i] = v;
-}
-
-// block q+1 from block q (slot `ps`) into slot `ns`.  Thread t < 227 makes words t, 227 + t and
-// 454 + t: each needs only the previous block and the thread's own earlier word (x_{k+624} =
-// x_{k+397} ^ twist(x_k, x_{k+1}); k + 397 - 624 is t, then 227 + t), so no barrier is needed
-// inside the block; word 623 also needs word 0, which thread 169 recomputes.
-__device__ __forceinline__ void mt_gen_block(uint32_t* ring, int ps, int ns) {
-    const int t = threadIdx.x;
+// block n (624 words) from block p.  Thread t < 227 makes words t, 227 + t and 454 + t: each needs
+// only block p and the thread's own earlier word (x_{k+624} = x_{k+397} ^ twist(x_k, x_{k+1}); k + 397
+// - 624 is t, then 227 + t), so no barrier is needed inside the block; word 623 also needs word 0 of
+// block n, which thread 169 recomputes.
+__device__ __forceinline__ void mt_next_block(const uint32_t* p, uint32_t* n, int t) {
     if (t < 227) {
-        const uint32_t* p = ring + ps * rtmt::N;
-        const uint32_t wa = rtmt::next_word(p[t], p[t + 1], p[t + 397]);
-        const uint32_t wb = rtmt::next_word(p[227 + t], p[228 + t], wa);
-        mt_store(ring, ns, t, wa);
-        mt_store(ring, ns, 227 + t, wb);
-        if (t < 170) {
-            const uint32_t x1 = (t == 169) ? rtmt::next_word(p[0], p[1], p[397]) : p[455 + t];
-            mt_store(ring, ns, 454 + t, rtmt::next_word(p[454 + t], x1, wb));
-        }
+        const uint32_t a0 = p[t], a1 = p[t + 1], a2 = p[t + 397], b0 = p[227 + t], b1 = p[228 + t];
+        const uint32_t c0 = t < 170 ? p[454 + t] : 0u;
+        uint32_t c1 = t < 169 ? p[455 + t] : 0u;
+        const uint32_t wa = rtmt::next_word(a0, a1, a2);
+        const uint32_t wb = rtmt::next_word(b0, b1, wa);
+        n[t] = wa;
+        n[227 + t] = wb;
+        if (t == 169) c1 = rtmt::next_word(p[0], p[1], p[397]);  // word 0 of block n
+        if (t < 170) n[454 + t] = rtmt::next_word(c0, c1, wb);
     }
 }
 
-// win <- p(T) win : out[m] = XOR_{i : p_i} y[i + m] with y generated forward from win (rt_mt.h).
-// Thread t owns m = t and t + MT_THREADS.  Set coefficient bits are taken four at a time with
-// scalar find-first-set and their eight LDS reads issued together (predicated when fewer remain).
-__device__ void mt_jump(uint32_t* win, uint32_t* ring, uint32_t* coef, const uint32_t* poly) {
-    const int t = threadIdx.x;
-    for (int m = t; m < rtmt::N; m += MT_THREADS) {
-        mt_store(ring, 0, m, win[m]);
-        coef[m] = poly[m];  // the 19937 coefficient bits, staged once (624 words)
-    }
-    __syncthreads();
-    mt_gen_block(ring, 0, 1);
-    mt_barrier();
-    const int m0 = t, m1 = t + MT_THREADS;  // m1 < 624 for t < 304
-    const int m1c = m1 < rtmt::N ? m1 : 0;
-    uint32_t acc0 = 0u, acc1 = 0u;
-    for (int b = 0; b * rtmt::N < rtmt::POLY_BITS; ++b) {
-        mt_gen_block(ring, (b + 1) % 3, (b + 2) % 3);  // block b + 2 (overwrites block b - 1)
-        const uint32_t* yb = ring + (b % 3) * rtmt::N;  // y[624 b + x], x < 1248
-        const int i0 = b * rtmt::N, i1 = min(i0 + rtmt::N, rtmt::POLY_BITS);
-        for (int wi = i0 >> 5; wi <= (i1 - 1) >> 5; ++wi) {
-            uint32_t w = __builtin_amdgcn_readfirstlane(coef[wi]);
-            const int lo = max(i0 - wi * 32, 0), hi = min(i1 - wi * 32, 32);
-            w &= (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-            const uint32_t* yw = yb + (wi * 32 - i0);
-            while (w) {
-                int k[4];
-                uint32_t keep[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    keep[u] = w ? 0xFFFFFFFFu : 0u;
-                    k[u] = w ? __builtin_ctz(w) : 0;
-                    w &= w - 1u;
-                }
-                uint32_t r0[4], r1[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    r0[u] = yw[k[u] + m0];
-                    r1[u] = yw[k[u] + m1c];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    acc0 ^= r0[u] & keep[u];
-                    acc1 ^= r1[u] & keep[u];
-                }
-            }
-        }
-        mt_barrier();
-    }
-    win[m0] = acc0;
-    if (m1 < rtmt::N) win[m1] = acc1;
-    mt_barrier();
-}
-
-// one workgroup per segment of the round: jump to the segment's window, generate its words,
-// write its doubles; the round's last segment hands the next round its key window, and the segment
-// holding the final state window copies it out
 __global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
-    __shared__ uint32_t win[rtmt::N];
-    __shared__ uint32_t ring[MT_SLOTS * rtmt::N];
-    __shared__ uint32_t coef[rtmt::N];
+    extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words (+ 624 coefficient words)
+    uint32_t* y = mt_lds;
+    uint32_t* coef = mt_lds + MT_YBLOCKS * rtmt::N;
+    uint32_t* ring = mt_lds;                    // 3 blocks, after the jump (aliases y)
+    uint32_t* red = mt_lds + 3 * rtmt::N;       // MT_WAVES x MT_RED (aliases y)
     const int s = blockIdx.x;
     const int t = threadIdx.x;
-    for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
-    __syncthreads();
-    if (s > 0) {
-        const int b = ((s - 1) % 16) + 1, a = (s - b) / 16;
-        mt_jump(win, ring, coef, A.tab + (int64_t)(b - 1) * rtmt::N);
-        if (a > 0) mt_jump(win, ring, coef, A.tab + (int64_t)(16 + a - 1) * rtmt::N);
-    }
     const int64_t ws = rtmt::window_start(s);
     const int64_t end = A.pos + A.words;  // round-relative, exclusive
     const int64_t lo = (int64_t)s * rtmt::L + A.pos;
     const int64_t hi = min((int64_t)(s + 1) * rtmt::L + A.pos, end);
-    int64_t gen_end = hi;
+    const int64_t npairs = hi > lo ? (hi - lo) / 2 : 0;
+    const int64_t dbase = A.double_base + (lo - A.pos) / 2;  // double of pair 0
+    // the pairs this segment stores: [0, kmax) minus the planes outside plane_mask; kend = one past
+    // the last stored pair (wave-uniform; a skipped draw is only stepped over)
+    const int kmax = (int)max<int64_t>(0, min<int64_t>(npairs, A.n_out - dbase));
+    int kend = kmax;
+    if (A.plane > 0 && kmax > 0) {
+        kend = 0;
+        for (int64_t pi = dbase / A.plane; pi * A.plane < dbase + kmax; ++pi)
+            if ((A.plane_mask >> (pi & 3)) & 1) kend = (int)min<int64_t>(kmax, (pi + 1) * A.plane - dbase);
+    }
+    int64_t gen_end = lo + 2 * (int64_t)kend;  // words to generate (exclusive)
     const bool chain = A.chain_dst && s == rtmt::SEGS - 1;
     const int64_t chain_at = rtmt::window_start(rtmt::SEGS);
     if (chain) gen_end = max(gen_end, chain_at + rtmt::N);
     const bool dump = A.dump_dst && rtmt::dumps(s, A.dump_at);
     if (dump) gen_end = max(gen_end, A.dump_at + rtmt::N);
-    for (int m = t; m < rtmt::N; m += MT_THREADS) mt_store(ring, 0, m, win[m]);
-    __syncthreads();
-    // output pairs are (pos + 2k, pos + 2k + 1); a block emits the pairs whose second word it holds
-    int64_t a_first = lo;
-    if (((a_first - A.pos) & 1) != 0) ++a_first;
-    for (int64_t q = 0; ws + q * rtmt::N < gen_end; ++q) {
-        const int slot = (int)(q % 3);
-        const int64_t b0 = ws + q * rtmt::N;  // absolute index of this block's first word
-        if (ws + (q + 1) * rtmt::N < gen_end) mt_gen_block(ring, slot, (slot + 1) % 3);
-        int64_t a0 = b0 - 1 > a_first ? b0 - 1 : a_first;
-        if (((a0 - A.pos) & 1) != 0) ++a0;
-        const int64_t a = a0 + 2 * t;
-        if (a + 1 < b0 + rtmt::N && a < hi) {
-            const int64_t d = A.double_base + (a - A.pos) / 2;
-            if (d < A.n_out) {
-                const int off = (int)(a - b0);  // -1: last word of the previous block
-                const uint32_t w0 = off >= 0 ? ring[slot * rtmt::N + off] : ring[((slot + 2) % 3) * rtmt::N + 623];
-                const uint32_t w1 = ring[slot * rtmt::N + off + 1];
-                A.out[d] = rtmt::to_double(rtmt::temper(w0), rtmt::temper(w1));
+    if (kend == 0 && !chain && !dump) return;  // nothing to store: the segment is stepped over
+    for (int m = t; m < rtmt::N; m += MT_THREADS) y[m] = A.key[m];
+    if (s > 0) {
+        const uint32_t* poly = A.tab + (int64_t)(s - 1) * rtmt::N;
+        for (int m = t; m < rtmt::N; m += MT_THREADS) coef[m] = poly[m];
+        __syncthreads();
+        for (int q = 0; q + 1 < MT_YBLOCKS; ++q) {
+            mt_next_block(y + q * rtmt::N, y + (q + 1) * rtmt::N, t);
+            mt_barrier();
+        }
+        const int wv = t >> 6, g = t & 63;
+        uint32_t acc[MT_G];
+#pragma unroll
+        for (int k = 0; k < MT_G; ++k) acc[k] = 0u;
+        for (int cw_i = wv * MT_CW_PER_WAVE; cw_i < (wv + 1) * MT_CW_PER_WAVE; ++cw_i) {
+            const uint32_t cw = __builtin_amdgcn_readfirstlane(coef[cw_i]);
+            if (cw == 0u) continue;
+            // y[32 cw_i + 10 g ...]: an even word index, so 8-byte aligned pair loads
+            const uint2* yp = reinterpret_cast<const uint2*>(y + 32 * cw_i + MT_G * g);
+            uint32_t r[32 + MT_G];
+#pragma unroll
+            for (int k = 0; k < (32 + MT_G) / 2; ++k) {
+                const uint2 v = yp[k];
+                r[2 * k] = v.x;
+                r[2 * k + 1] = v.y;
             }
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                if (cw & (1u << j)) {  // wave-uniform
+#pragma unroll
+                    for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + k];
+                }
+            }
+        }
+        __syncthreads();  // every wave is done reading y
+#pragma unroll
+        for (int k = 0; k < MT_G; ++k) red[wv * MT_RED + MT_G * g + k] = acc[k];
+        __syncthreads();
+        for (int m = t; m < rtmt::N; m += MT_THREADS) {
+            uint32_t w = 0u;
+#pragma unroll
+            for (int v = 0; v < MT_WAVES; ++v) w ^= red[v * MT_RED + m];
+            ring[m] = w;
+        }
+    }
+    __syncthreads();
+    // generation: block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it
+    // holds
+    const int off0 = (int)(lo - ws);    // 1 .. 625 (s > 0) or pos (s == 0)
+    const int c0 = -((off0 + 1) >> 1);  // pair index of block 0's first pair
+    const int o = off0 + 2 * (c0 + t);  // in-block offset of this thread's first word: -1 .. 622
+    double* outp = A.out + dbase;
+    // plane of pair k: pidx while k < kb, then pidx + 1 (a block's 312 pairs span at most two planes)
+    int64_t pidx = 0, kb = INT64_MAX;
+    if (A.plane > 0) {
+        pidx = dbase / A.plane;
+        kb = (pidx + 1) * A.plane - dbase;
+    }
+    int kq = c0;  // pair of thread 0 in block q
+    int slot = 0, prev = 2, next = 1;
+    for (int64_t b0 = ws; b0 < gen_end; b0 += rtmt::N) {
+        uint32_t* cur = ring + slot * rtmt::N;
+        if (b0 + rtmt::N < gen_end) mt_next_block(cur, ring + next * rtmt::N, t);
+        if (kq >= kb) {
+            ++pidx;
+            kb += A.plane;
+        }
+        const int k = kq + t;
+        if (t < 312 && k >= 0 && k < kend &&
+            (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1))) {
+            const uint32_t w0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
+            const uint32_t w1 = cur[o + 1];
+            outp[k] = rtmt::to_double(rtmt::temper(w0), rtmt::temper(w1));
         }
         if (chain || dump) {
             for (int m = t; m < rtmt::N; m += MT_THREADS) {
                 const int64_t x = b0 + m;
-                const uint32_t v = ring[slot * rtmt::N + m];
+                const uint32_t v = cur[m];
                 if (chain && x >= chain_at && x < chain_at + rtmt::N) A.chain_dst[x - chain_at] = v;
                 if (dump && x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = v;
             }
         }
+        kq += 312;
+        prev = slot;
+        slot = next;
+        next = next == 2 ? 0 : next + 1;
         mt_barrier();
     }
 }
@@ -1078,6 +1092,12 @@ constexpr int FRAME_SLOTS = RT_FRAME_SLOTS;
 // ex1 1080p (ms/frame): 1 slot 1.47, 2 slots 1.308, 3 slots 1.292; 1/8 shard 0.28 / 0.202 / 0.199.
 struct FrameSlot {
     hipStream_t stream = nullptr;
+    // host outputs of an asynchronous frame are copied on a stream of their own, so the next frame
+    // on this slot computes while they cross PCIe; only its resolve (which rewrites rgb / u8) waits
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t resolved = nullptr;   // recorded on `stream` after the frame's outputs are final
+    hipEvent_t copied = nullptr;     // recorded on `copy_stream` after their copies
+    bool copy_pending = false;       // `copied` guards rgb / u8 of this slot
     // ray queues: 2 x NSHARD segments of `seg` rays
     Queue q[2]{};
     int64_t seg = 0;
@@ -1374,12 +1394,15 @@ int64_t depth_total(const uint32_t* cnt, int64_t seg) {
 namespace {
 
 // ---- numpy's stream on the device (rt_mt.h): scratch c->mt = jump tables | key 0 | key 1 | dump ----
-constexpr int64_t MT_NTAB = 31 * rtmt::N;
+constexpr int64_t MT_NTAB = rtmt::TABLE_WORDS;
+constexpr size_t MT_LDS_BYTES = (size_t)(MT_YBLOCKS + 1) * rtmt::N * 4;
 uint32_t* mt_key0(srt_ctx* c) { return c->mt + MT_NTAB; }
 uint32_t* mt_dump(srt_ctx* c) { return c->mt + MT_NTAB + 2 * rtmt::N; }
 
 int mt_ensure(srt_ctx* c) {
     if (c->mt) return SRT_OK;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_round),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)MT_LDS_BYTES));
     HIP_TRY(dalloc(&c->mt, MT_NTAB + 3 * rtmt::N));
     HIP_TRY(hipMemcpy(c->mt, rtmt::tables_flat(), MT_NTAB * 4, hipMemcpyHostToDevice));
     return SRT_OK;
@@ -1387,8 +1410,10 @@ int mt_ensure(srt_ctx* c) {
 
 // Queue on `st`: from the key window in mt_key0 at position `pos`, n_out doubles into `out` (device)
 // and n_skip more draws; the window holding the last consumed word goes to mt_dump.  Returns the
-// numpy position of that window in *final_pos.
-int mt_launch(srt_ctx* c, hipStream_t st, int pos, int64_t n_out, int64_t n_skip, double* out, int* final_pos) {
+// numpy position of that window in *final_pos.  `plane` > 0: only the doubles of the planes
+// (index % 4) in `plane_mask` are stored (a pinhole camera reads no lens-disk pair).
+int mt_launch(srt_ctx* c, hipStream_t st, int pos, int64_t n_out, int64_t n_skip, double* out, int* final_pos,
+              int64_t plane = 0, int plane_mask = 15) {
     uint32_t* keys[2] = {c->mt + MT_NTAB, c->mt + MT_NTAB + rtmt::N};
     const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
     for (size_t r = 0; r < plan.rounds.size(); ++r) {
@@ -1404,7 +1429,10 @@ int mt_launch(srt_ctx* c, hipStream_t st, int pos, int64_t n_out, int64_t n_skip
         A.n_out = n_out;
         A.dump_at = R.dump_at;
         A.pos = R.pos;
-        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), 0, st, A);
+        // the block's doubles span at most two planes when a plane holds >= 312 of them
+        A.plane = plane >= 1024 ? plane : 0;
+        A.plane_mask = plane_mask;
+        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), MT_LDS_BYTES, st, A);
         HIP_TRY(hipGetLastError());
     }
     *final_pos = plan.final_pos;
@@ -1477,6 +1505,9 @@ void clear_host_flags(srt_ctx* c, const FramePlan& F) {
 int ensure_slot(FrameSlot& f) {
     if (f.stream) return SRT_OK;
     HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&f.copy_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&f.resolved, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&f.copied, hipEventDisableTiming));
     HIP_TRY(dalloc(&f.counts, SRT_MAX_DEPTHS * NSHARD));
     HIP_TRY(dalloc(&f.flags, 2));
     HIP_TRY(dalloc(&f.shadow, NSHARD));
@@ -1487,6 +1518,7 @@ int ensure_slot(FrameSlot& f) {
 void free_slot(FrameSlot& f) {
     if (!f.stream) return;
     (void)hipStreamSynchronize(f.stream);
+    (void)hipStreamSynchronize(f.copy_stream);
     free_list(f.queue_bufs);
     free_list(f.ring_bufs);
     void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb};
@@ -1494,6 +1526,9 @@ void free_slot(FrameSlot& f) {
         if (p) (void)hipFree(p);
     for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     if (f.host) (void)hipHostFree(f.host);
+    (void)hipEventDestroy(f.resolved);
+    (void)hipEventDestroy(f.copied);
+    (void)hipStreamDestroy(f.copy_stream);
     (void)hipStreamDestroy(f.stream);
     f = FrameSlot{};
 }
@@ -1508,7 +1543,11 @@ int finish_async(srt_ctx* c, srt_stats* st) {
         return SRT_OK;
     }
     for (FrameSlot& f : c->slots)
-        if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
+        if (f.stream) {
+            HIP_TRY(hipStreamSynchronize(f.stream));
+            HIP_TRY(hipStreamSynchronize(f.copy_stream));
+            f.copy_pending = false;
+        }
     c->async_pending = 0;
     if (c->mt_chain) {  // numpy's state after the last asynchronous frame's draws
         HIP_TRY(hipMemcpy(c->mt_chain->key, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost));
@@ -2036,7 +2075,12 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 const int64_t n_skip = (p + 1 == F.npass) ? 4 * W * Hf : 0;
                 if (p > 0)
                     HIP_TRY(hipMemcpyAsync(mt_key0(c), mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToDevice, c->f->stream));
-                if ((rc = mt_launch(c, c->f->stream, mt_pos, n_out, n_skip, c->f->jit, &mt_pos))) return rc;
+                // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
+                if ((rc = mt_launch(c, c->f->stream, mt_pos, n_out, n_skip, c->f->jit, &mt_pos, W * Hf,
+                                    cam->lens_radius != 0.0 ? 15 : 3)))
+                    return rc;
+                // the next frame's stream may start as soon as this one's is generated
+                if (p + 1 == F.npass) HIP_TRY(hipEventRecord(c->mt_done, c->f->stream));
                 P.jitter = c->f->jit;
                 P.jit_plane = W * Hf;
                 P.jit_global = 1;
@@ -2063,6 +2107,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 P.out_rgb = res_rgb;
                 P.out_u8 = res_u8;
                 P.spp_total = a->spp;
+                // (the fused resolve rewrites rgb / u8: the previous frame's copies from them first)
+                if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
                 HIP_TRY(hipEventRecord(ev[0], c->f->stream));
                 hipLaunchKernelGGL(V.frame, dim3((unsigned)((npix + FRAME_BLOCK - 1) / FRAME_BLOCK)), dim3(FRAME_BLOCK),
                                    lut_bytes(c), c->f->stream, P);
@@ -2109,14 +2155,12 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 HIP_TRY(hipMemcpyAsync(a->out_hit_id + (int64_t)s0 * npix, c->f->hit, (size_t)nrays * 4,
                                        hipMemcpyDeviceToHost, c->f->stream));
         }
-        if (use_mt) {
-            HIP_TRY(hipEventRecord(c->mt_done, c->f->stream));
-            c->mt_pos = mt_pos;
-        }
+        if (use_mt) c->mt_pos = mt_pos;
         uint32_t* hshadow = c->f->host + F.npass * F.pass_words;
         // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
         const bool fused = F.frame && F.npass == 1;
         uint32_t* hlast = c->f->host + (F.npass - 1) * F.pass_words;
+        if (c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
         hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
                            fused ? (int64_t)0 : npix, c->f->shadow, hshadow, (double)a->spp, res_rgb, res_u8, c->f->counts,
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
@@ -2145,11 +2189,17 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             if (sharded && !c->defer_gather && (rc = gather_frame(c))) return rc;
             // host outputs (pinned) are copied on the frame's stream; stats and errors come with
             // srt_render_finish; the next asynchronous frame goes to the next slot
-            if (!sharded) {
-                if (a->out_rgb && !rgb_dev)
-                    HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->f->stream));
+            if (!sharded && ((a->out_rgb && !rgb_dev) || (a->out_srgb8 && !u8_dev))) {
+                HIP_TRY(hipEventRecord(c->f->resolved, c->f->stream));
+                HIP_TRY(hipStreamWaitEvent(c->f->copy_stream, c->f->resolved, 0));
                 if (a->out_srgb8 && !u8_dev)
-                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->f->stream));
+                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost,
+                                           c->f->copy_stream));
+                if (a->out_rgb && !rgb_dev)
+                    HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost,
+                                           c->f->copy_stream));
+                HIP_TRY(hipEventRecord(c->f->copied, c->f->copy_stream));
+                c->f->copy_pending = true;
             }
             if (use_mt) c->mt_chain = a->mt;
             c->async_pending++;

@@ -9,14 +9,14 @@
 //
 // The word stream is cut into segments of L = 2^19 words.  Segment s starts from the window
 // W_{sL-1} = p(T) W_0 with p(x) = x^(sL-1) mod phi(x) (phi: characteristic polynomial of the
-// transition T, tables in rt_mt_jump.h), evaluated without polynomial arithmetic as
+// transition T; one tabulated polynomial per segment of a round, rt_mt_jump.h), evaluated without polynomial arithmetic as
 //     W'[m] = XOR_{i : p_i = 1} y[i + m],   y = the raw words generated forward from W_0.
 // T is singular: its kernel K is the low 31 bits of a window's first word (they never influence
 // later words).  Writing W_0 = v + k (v in Im T, k in K), p(T) W_0 = T^J v + p_0 k, so a jumped
 // window is exact except the low 31 bits of its first word -- which a segment never outputs (its
 // outputs start at least one word later) and never dumps.
 //
-// Rounds: one launch covers up to RT_MT_SEGS segments (RT_MT_SEGS * L words); the next round starts
+// Rounds: one launch covers up to SEGS segments (SEGS * L words); the next round starts
 // from the exact window at the last segment's end.  The final numpy state is the window that
 // contains the last consumed word, dumped by the segment that generates it.
 #pragma once
@@ -32,7 +32,7 @@ constexpr int N = 624;
 constexpr int M = 397;
 constexpr uint32_t MATRIX_A = 0x9908B0DFu, UPPER = 0x80000000u, LOWER = 0x7FFFFFFFu;
 constexpr int64_t L = (int64_t)1 << RT_MT_SEG_LOG2;  // words per segment
-constexpr int SEGS = 256;                             // segments per round (two-level jump table)
+constexpr int SEGS = 256;                             // segments per round (one jump polynomial each)
 constexpr int POLY_BITS = 19937;
 
 #if defined(__HIPCC__)
@@ -59,27 +59,13 @@ RT_MT_HD double to_double(uint32_t w0, uint32_t w1) {
     return ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) / 9007199254740992.0;
 }
 
-// jump polynomials for segment s >= 1 of a round: window at s*L - 1 from the round's key window.
-// sL - 1 = a*16L + (bL - 1), b = ((s-1) % 16) + 1 in [1,16], a in [0,15]
-struct JumpPlan {
-    const uint32_t* first;   // x^(bL-1)
-    const uint32_t* second;  // x^(16aL) or null
-};
-inline JumpPlan jump_plan(int s) {
-    const int b = ((s - 1) % 16) + 1;
-    const int a = (s - b) / 16;
-    return JumpPlan{RT_MT_J1[b - 1], a > 0 ? RT_MT_J2[a - 1] : nullptr};
-}
+// jump polynomial of segment s in [1, SEGS) of a round: x^(sL-1), the window at s*L - 1 from the
+// round's key window
+inline const uint32_t* jump_poly(int s) { return RT_MT_JD[s - 1]; }
 
-// J1 then J2 as one array (device upload)
-inline const uint32_t* tables_flat() {
-    static std::vector<uint32_t> t;
-    if (t.empty()) {
-        t.insert(t.end(), &RT_MT_J1[0][0], &RT_MT_J1[0][0] + 16 * N);
-        t.insert(t.end(), &RT_MT_J2[0][0], &RT_MT_J2[0][0] + 15 * N);
-    }
-    return t.data();
-}
+// the whole table as one array (device upload): (SEGS - 1) x 624 words
+inline const uint32_t* tables_flat() { return &RT_MT_JD[0][0]; }
+constexpr int64_t TABLE_WORDS = (int64_t)(SEGS - 1) * N;
 
 // absolute (round-relative) word index where segment s's window starts
 RT_MT_HD int64_t window_start(int s) { return s == 0 ? 0 : (int64_t)s * L - 1; }
@@ -182,13 +168,7 @@ inline void uniforms_serial(const uint32_t* key, int pos, int64_t n_out, int64_t
             if (s == 0) {
                 w = rkey;
             } else {
-                const JumpPlan J = jump_plan(s);
-                jump_serial(rkey.data(), J.first, w.data());
-                if (J.second) {
-                    std::vector<uint32_t> w2(N);
-                    jump_serial(w.data(), J.second, w2.data());
-                    w = w2;
-                }
+                jump_serial(rkey.data(), jump_poly(s), w.data());
             }
             SerialStream g(w.data());
             const int64_t ws = window_start(s);

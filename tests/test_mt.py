@@ -32,7 +32,7 @@ CASES = [
     (3, 312, 1, 0),              # pos = 624 after draws
     (4, 5, 2 * L_DOUBLES + 17, 100),   # three segments (jumps x^(L-1), x^(2L-1))
     (5, 100, L_DOUBLES - 1, 2),  # ends right at a segment boundary
-    (6, 7, 100, 17 * L_DOUBLES),  # skipped draws cross 17 segments (second-level jump)
+    (6, 7, 100, 17 * L_DOUBLES),  # skipped draws cross 17 segments
     (7, 3, 256 * L_DOUBLES + 1000, 5),  # outputs cross a round (256 segments): chained key window
     (8, 620, 40, 256 * L_DOUBLES - 45),  # final state window lands in the previous round
 ]
@@ -54,14 +54,13 @@ def test_jump_table_is_the_mt19937_jump():
     src = (ROOT / "python-raytracer_amd" / "csrc" / "rt_mt_jump.h").read_text()
     import re
 
-    def table(name):
-        body = src.split("static const uint32_t %s" % name)[1].split("};")[0]
-        return [sum(int(v, 16) << (32 * k) for k, v in enumerate(r.split(",")))
-                for r in re.findall(r"\{(0x[^{}]*)\}", body)]
-
-    j1 = table("RT_MT_J1")
-    assert len(j1) == 16 and len(table("RT_MT_J2")) == 15
-    G.check_jump(j1[0], G.L - 1)
+    body = src.split("static const uint32_t RT_MT_JD")[1].split("};")[0]
+    rows = re.findall(r"\{(0x[^{}]*)\}", body)
+    assert len(rows) == 255
+    jd = [sum(int(v, 16) << (32 * k) for k, v in enumerate(r.split(","))) for r in (rows[0], rows[1])]
+    G.check_jump(jd[0], G.L - 1)
+    # consecutive entries differ by x^L: the second is x^(2L-1) (checked by its window)
+    G.check_jump(jd[1], 2 * G.L - 1)
 
 
 def _device_uniforms(st, n_out, n_skip, device_out=False):

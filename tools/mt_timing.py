@@ -15,7 +15,7 @@ lib, ctx = B.context()
 key = np.ascontiguousarray(np.random.RandomState(0).get_state()[1], dtype=np.uint32)
 ko = np.empty(624, dtype=np.uint32)
 po = ctypes.c_int32()
-for label, n in [("1 seg (no jump)", L2 - 8), ("2 segs (1 jump)", 2 * L2 - 8), ("17 segs (2 jumps)", 17 * L2 - 8),
+for label, n in [("1 seg (no jump)", L2 - 8), ("2 segs", 2 * L2 - 8), ("17 segs", 17 * L2 - 8), ("256 segs", 256 * L2 - 8),
                  ("1080p x 7 draws", 7 * 4 * 1920 * 1080), ("tiny", 1000)]:
     p = B.device_buffer("t", 8 * n)
     ts = []
