@@ -30,8 +30,10 @@
 #include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_mt.h"
+#include "rt_mt_kernel.h"
 
 using namespace rt;
+using namespace rtmt_dev;
 
 namespace {
 
@@ -499,6 +501,23 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
 // (simulated on the ex1 1080p path-length distribution: 94.6 % with pure chunks).
 constexpr int FRAME_BLOCK = 64;
 
+// The uint8 RGB of 64 consecutive pixels (lane l holds pixel p0 + l; dst = out + 3 p0) as 48 dword
+// stores instead of 192 byte stores.  `n` < 64 pixels (the frame's last chunk) or an unaligned dst store bytes.  Every lane
+// of the wave must call it (cross-lane reads).
+__device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3], int lane, int n) {
+    const uint32_t v = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+    if (n == 64 && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+        const int w = lane < 48 ? lane : 47;
+        const int q0 = (4 * w) / 3, r0 = (4 * w) % 3;  // dword w = bytes 4w..4w+3: pixels q0, q0 + 1
+        const uint32_t x0 = __shfl(v, q0), x1 = __shfl(v, q0 + 1);
+        if (lane < 48) reinterpret_cast<uint32_t*>(dst)[lane] = (x0 >> (8 * r0)) | (x1 << (8 * (3 - r0)));
+    } else if (lane < n) {
+        dst[3 * lane] = px[0];
+        dst[3 * lane + 1] = px[1];
+        dst[3 * lane + 2] = px[2];
+    }
+}
+
 struct FrameLds {
     double acc[3][FRAME_BLOCK];  // per-pixel colour sums of the tile
     uint32_t depth_cnt[SRT_MAX_DEPTHS];
@@ -669,17 +688,22 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     }
     RT_T0(te0);
     // tile pixels out
-    if (pact) {
-        const double ar = L.acc[0][lane], ag = L.acc[1][lane], ab = L.acc[2][lane];
-        if (P.fuse_resolve) {
+    if (P.fuse_resolve) {
+        uint8_t px[3] = {0, 0, 0};
+        if (pact) {
             const double spp = (double)P.spp_total;
-            double rr = ar / spp, gg = ag / spp, bb = ab / spp;
-            uint8_t px[3];
+            double rr = L.acc[0][lane] / spp, gg = L.acc[1][lane] / spp, bb = L.acc[2][lane] / spp;
             double a0, a1, a2;
             resolve_pixel(rr, gg, bb, a0, a1, a2, px);
             if (P.out_rgb) { P.out_rgb[p] = rr; P.out_rgb[P.npix + p] = gg; P.out_rgb[2 * P.npix + p] = bb; }
-            if (P.out_u8) { P.out_u8[3 * p] = px[0]; P.out_u8[3 * p + 1] = px[1]; P.out_u8[3 * p + 2] = px[2]; }
-        } else if (P.fb_first) {
+        }
+        if (P.out_u8) {
+            const int64_t p0 = p - lane;
+            store_u8_chunk(P.out_u8 + 3 * p0, px, lane, (int)min<int64_t>(64, P.npix - p0));
+        }
+    } else if (pact) {
+        const double ar = L.acc[0][lane], ag = L.acc[1][lane], ab = L.acc[2][lane];
+        if (P.fb_first) {
             P.fb[p] = ar; P.fb[P.npix + p] = ag; P.fb[2 * P.npix + p] = ab;
         } else {
             P.fb[p] += ar; P.fb[P.npix + p] += ag; P.fb[2 * P.npix + p] += ab;
@@ -782,13 +806,19 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npi
             shadow_host[1] = (uint32_t)(v >> 32);
         }
     }
-    for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK) {
-        double r = fb[p] / spp, g = fb[npix + p] / spp, b = fb[2 * npix + p] / spp;
-        uint8_t px[3];
-        double a0, a1, a2;
-        resolve_pixel(r, g, b, a0, a1, a2, px);
-        if (rgb) { rgb[p] = r; rgb[npix + p] = g; rgb[2 * npix + p] = b; }
-        if (u8) { u8[3 * p] = px[0]; u8[3 * p + 1] = px[1]; u8[3 * p + 2] = px[2]; }
+    // wave-uniform trip count: each wave takes 64 consecutive pixels per step
+    const int lane = threadIdx.x & 63;
+    for (int64_t p0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); p0 < npix; p0 += (int64_t)gridDim.x * BLOCK) {
+        const int64_t p = p0 + lane;
+        const int n = (int)min<int64_t>(64, npix - p0);
+        uint8_t px[3] = {0, 0, 0};
+        if (p < npix) {
+            double r = fb[p] / spp, g = fb[npix + p] / spp, b = fb[2 * npix + p] / spp;
+            double a0, a1, a2;
+            resolve_pixel(r, g, b, a0, a1, a2, px);
+            if (rgb) { rgb[p] = r; rgb[npix + p] = g; rgb[2 * npix + p] = b; }
+        }
+        if (u8) store_u8_chunk(u8 + 3 * p0, px, lane, n);
     }
 }
 
@@ -892,182 +922,6 @@ __global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, cons
 }
 
 
-// ---- numpy legacy RNG stream on the device (rt_mt.h) ---------------------------------------------
-struct MtArgs {
-    const uint32_t* key;   // the round's key window (624 words)
-    const uint32_t* tab;   // jump polynomials x^(sL-1), s = 1..SEGS-1 (624 words each)
-    double* out;           // doubles of the whole call
-    uint32_t* chain_dst;   // next round's key window (written by segment SEGS-1) or null
-    uint32_t* dump_dst;    // final numpy key window or null
-    int64_t words;         // words consumed by this round
-    int64_t double_base;   // first double of this round
-    int64_t n_out;         // doubles to write (the rest are skipped draws)
-    int64_t dump_at;       // round-relative start of the final state window, or -1
-    int64_t plane;         // doubles per jitter plane (0: write every double)
-    int32_t plane_mask;    // bit k set: write the doubles of planes with index % 4 == k
-    int32_t pos;           // outputs start at word `pos` of the key window
-};
-
-// One workgroup per segment.  Jump: y = the 34 x 624 raw words generated from the key window (LDS),
-// then W'[m] = XOR_{i : p_i} y[i + m] -- wave v takes coefficient words [78 v, 78 v + 78), lane g the
-// ten outputs m = 10 g .. 10 g + 9 with y[32 w + 10 g .. + 41] in registers, so a set bit costs ten
-// register XORs and no LDS traffic; the eight waves' partial windows are XOR-reduced through LDS.
-// Generation: a ring of three 624-word blocks; threads < 227 make the next block (three dependent
-// words each) while threads < 312 temper and store the current block's 312 doubles.
-constexpr int MT_THREADS = 512;
-constexpr int MT_WAVES = MT_THREADS / 64;
-constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 78 coefficient words
-constexpr int MT_G = 10;                              // window outputs per lane in the jump
-constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
-constexpr int MT_RED = 640;                           // per-wave stride of the reduction buffer
-static_assert(MT_CW_PER_WAVE * MT_WAVES == rtmt::N, "coefficient words split evenly over the waves");
-static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 42 <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
-static_assert(3 * rtmt::N + MT_WAVES * MT_RED <= MT_YBLOCKS * rtmt::N, "ring and reduction alias y");
-
-// workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic, not for its global
-// stores (__syncthreads() would also drain the output stores every block)
-__device__ __forceinline__ void mt_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
-    __builtin_amdgcn_s_barrier();
-}
-
-// block n (624 words) from block p.  Thread t < 227 makes words t, 227 + t and 454 + t: each needs
-// only block p and the thread's own earlier word (x_{k+624} = x_{k+397} ^ twist(x_k, x_{k+1}); k + 397
-// - 624 is t, then 227 + t), so no barrier is needed inside the block; word 623 also needs word 0 of
-// block n, which thread 169 recomputes.
-__device__ __forceinline__ void mt_next_block(const uint32_t* p, uint32_t* n, int t) {
-    if (t < 227) {
-        const uint32_t a0 = p[t], a1 = p[t + 1], a2 = p[t + 397], b0 = p[227 + t], b1 = p[228 + t];
-        const uint32_t c0 = t < 170 ? p[454 + t] : 0u;
-        uint32_t c1 = t < 169 ? p[455 + t] : 0u;
-        const uint32_t wa = rtmt::next_word(a0, a1, a2);
-        const uint32_t wb = rtmt::next_word(b0, b1, wa);
-        n[t] = wa;
-        n[227 + t] = wb;
-        if (t == 169) c1 = rtmt::next_word(p[0], p[1], p[397]);  // word 0 of block n
-        if (t < 170) n[454 + t] = rtmt::next_word(c0, c1, wb);
-    }
-}
-
-__global__ __launch_bounds__(MT_THREADS) void k_mt_round(MtArgs A) {
-    extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words (+ 624 coefficient words)
-    uint32_t* y = mt_lds;
-    uint32_t* coef = mt_lds + MT_YBLOCKS * rtmt::N;
-    uint32_t* ring = mt_lds;                    // 3 blocks, after the jump (aliases y)
-    uint32_t* red = mt_lds + 3 * rtmt::N;       // MT_WAVES x MT_RED (aliases y)
-    const int s = blockIdx.x;
-    const int t = threadIdx.x;
-    const int64_t ws = rtmt::window_start(s);
-    const int64_t end = A.pos + A.words;  // round-relative, exclusive
-    const int64_t lo = (int64_t)s * rtmt::L + A.pos;
-    const int64_t hi = min((int64_t)(s + 1) * rtmt::L + A.pos, end);
-    const int64_t npairs = hi > lo ? (hi - lo) / 2 : 0;
-    const int64_t dbase = A.double_base + (lo - A.pos) / 2;  // double of pair 0
-    // the pairs this segment stores: [0, kmax) minus the planes outside plane_mask; kend = one past
-    // the last stored pair (wave-uniform; a skipped draw is only stepped over)
-    const int kmax = (int)max<int64_t>(0, min<int64_t>(npairs, A.n_out - dbase));
-    int kend = kmax;
-    if (A.plane > 0 && kmax > 0) {
-        kend = 0;
-        for (int64_t pi = dbase / A.plane; pi * A.plane < dbase + kmax; ++pi)
-            if ((A.plane_mask >> (pi & 3)) & 1) kend = (int)min<int64_t>(kmax, (pi + 1) * A.plane - dbase);
-    }
-    int64_t gen_end = lo + 2 * (int64_t)kend;  // words to generate (exclusive)
-    const bool chain = A.chain_dst && s == rtmt::SEGS - 1;
-    const int64_t chain_at = rtmt::window_start(rtmt::SEGS);
-    if (chain) gen_end = max(gen_end, chain_at + rtmt::N);
-    const bool dump = A.dump_dst && rtmt::dumps(s, A.dump_at);
-    if (dump) gen_end = max(gen_end, A.dump_at + rtmt::N);
-    if (kend == 0 && !chain && !dump) return;  // nothing to store: the segment is stepped over
-    for (int m = t; m < rtmt::N; m += MT_THREADS) y[m] = A.key[m];
-    if (s > 0) {
-        const uint32_t* poly = A.tab + (int64_t)(s - 1) * rtmt::N;
-        for (int m = t; m < rtmt::N; m += MT_THREADS) coef[m] = poly[m];
-        __syncthreads();
-        for (int q = 0; q + 1 < MT_YBLOCKS; ++q) {
-            mt_next_block(y + q * rtmt::N, y + (q + 1) * rtmt::N, t);
-            mt_barrier();
-        }
-        const int wv = t >> 6, g = t & 63;
-        uint32_t acc[MT_G];
-#pragma unroll
-        for (int k = 0; k < MT_G; ++k) acc[k] = 0u;
-        for (int cw_i = wv * MT_CW_PER_WAVE; cw_i < (wv + 1) * MT_CW_PER_WAVE; ++cw_i) {
-            const uint32_t cw = __builtin_amdgcn_readfirstlane(coef[cw_i]);
-            if (cw == 0u) continue;
-            // y[32 cw_i + 10 g ...]: an even word index, so 8-byte aligned pair loads
-            const uint2* yp = reinterpret_cast<const uint2*>(y + 32 * cw_i + MT_G * g);
-            uint32_t r[32 + MT_G];
-#pragma unroll
-            for (int k = 0; k < (32 + MT_G) / 2; ++k) {
-                const uint2 v = yp[k];
-                r[2 * k] = v.x;
-                r[2 * k + 1] = v.y;
-            }
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                if (cw & (1u << j)) {  // wave-uniform
-#pragma unroll
-                    for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + k];
-                }
-            }
-        }
-        __syncthreads();  // every wave is done reading y
-#pragma unroll
-        for (int k = 0; k < MT_G; ++k) red[wv * MT_RED + MT_G * g + k] = acc[k];
-        __syncthreads();
-        for (int m = t; m < rtmt::N; m += MT_THREADS) {
-            uint32_t w = 0u;
-#pragma unroll
-            for (int v = 0; v < MT_WAVES; ++v) w ^= red[v * MT_RED + m];
-            ring[m] = w;
-        }
-    }
-    __syncthreads();
-    // generation: block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it
-    // holds
-    const int off0 = (int)(lo - ws);    // 1 .. 625 (s > 0) or pos (s == 0)
-    const int c0 = -((off0 + 1) >> 1);  // pair index of block 0's first pair
-    const int o = off0 + 2 * (c0 + t);  // in-block offset of this thread's first word: -1 .. 622
-    double* outp = A.out + dbase;
-    // plane of pair k: pidx while k < kb, then pidx + 1 (a block's 312 pairs span at most two planes)
-    int64_t pidx = 0, kb = INT64_MAX;
-    if (A.plane > 0) {
-        pidx = dbase / A.plane;
-        kb = (pidx + 1) * A.plane - dbase;
-    }
-    int kq = c0;  // pair of thread 0 in block q
-    int slot = 0, prev = 2, next = 1;
-    for (int64_t b0 = ws; b0 < gen_end; b0 += rtmt::N) {
-        uint32_t* cur = ring + slot * rtmt::N;
-        if (b0 + rtmt::N < gen_end) mt_next_block(cur, ring + next * rtmt::N, t);
-        if (kq >= kb) {
-            ++pidx;
-            kb += A.plane;
-        }
-        const int k = kq + t;
-        if (t < 312 && k >= 0 && k < kend &&
-            (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1))) {
-            const uint32_t w0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
-            const uint32_t w1 = cur[o + 1];
-            outp[k] = rtmt::to_double(rtmt::temper(w0), rtmt::temper(w1));
-        }
-        if (chain || dump) {
-            for (int m = t; m < rtmt::N; m += MT_THREADS) {
-                const int64_t x = b0 + m;
-                const uint32_t v = cur[m];
-                if (chain && x >= chain_at && x < chain_at + rtmt::N) A.chain_dst[x - chain_at] = v;
-                if (dump && x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = v;
-            }
-        }
-        kq += 312;
-        prev = slot;
-        slot = next;
-        next = next == 2 ? 0 : next + 1;
-        mt_barrier();
-    }
-}
-
 }  // namespace
 
 // shape of one frame's passes (what the read-back of its counters needs)
@@ -1081,23 +935,23 @@ struct FramePlan {
     int64_t cnt_words = 0, pass_words = 0;
 };
 
-#ifndef RT_FRAME_SLOTS
-#define RT_FRAME_SLOTS 3
-#endif
-constexpr int FRAME_SLOTS = RT_FRAME_SLOTS;
+constexpr int MAX_FRAME_SLOTS = 4;
 
 // Buffers and stream of one frame in flight.  Synchronous calls use slot 0; pipelined
 // (SRT_RENDER_ASYNC) frames rotate over the slots, each with its own stream, so one frame's
 // low-occupancy tail (deep depths, resolve) overlaps the next frame's primary kernel.  Measured on
-// ex1 1080p (ms/frame): 1 slot 1.47, 2 slots 1.308, 3 slots 1.292; 1/8 shard 0.28 / 0.202 / 0.199.
+// ex1 1080p (ms/frame, device-resident): 1 slot 1.47, 2 slots 1.308, 3 slots 1.292; 1/8 shard 0.28 /
+// 0.202 / 0.199.  The slot count, the generation stream and a separate copy stream are options
+// (srt_set_option "slots", "mt_stream", "copy_stream"): HIP gives a process four hardware queues by
+// default, and a stream that shares a queue with another waits behind that stream's work.
 struct FrameSlot {
     hipStream_t stream = nullptr;
-    // host outputs of an asynchronous frame are copied on a stream of their own, so the next frame
-    // on this slot computes while they cross PCIe; only its resolve (which rewrites rgb / u8) waits
-    hipStream_t copy_stream = nullptr;
     hipEvent_t resolved = nullptr;   // recorded on `stream` after the frame's outputs are final
-    hipEvent_t copied = nullptr;     // recorded on `copy_stream` after their copies
+    hipEvent_t copied = nullptr;     // recorded on the copy stream after their host copies
     bool copy_pending = false;       // `copied` guards rgb / u8 of this slot
+    hipEvent_t jit_ready = nullptr;  // recorded on the MT stream after this slot's jitter is generated
+    hipEvent_t jit_free = nullptr;   // recorded on `stream` after the last kernel that reads the jitter
+    bool jit_busy = false;           // `jit_free` guards the jitter buffer
     // ray queues: 2 x NSHARD segments of `seg` rays
     Queue q[2]{};
     int64_t seg = 0;
@@ -1174,7 +1028,7 @@ struct srt_ctx {
     int32_t* rows = nullptr;
     int64_t cam_cap[3] = {0, 0, 0};
     std::vector<uint8_t> cam_host[3];  // host copies of what xs / ys / rows hold
-    uint32_t* mt = nullptr;    // MT19937 jump tables (31 x 624) + two round keys + the final key
+    uint32_t* mt = nullptr;    // MT19937 jump tables (255 x 624), two round keys, two final windows, segment windows
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
@@ -1190,7 +1044,16 @@ struct srt_ctx {
     int64_t hint_key[3] = {-1, -1, -1};
     int64_t hint[SRT_MAX_DEPTHS] = {};
     // frame slots; `f` is the one the current call works on
-    FrameSlot slots[FRAME_SLOTS];
+    FrameSlot slots[MAX_FRAME_SLOTS];
+    // pipelined frames: slots they rotate over (option "slots"); the numpy-stream generation of
+    // single-pass frames on a stream of its own ("mt_stream"); host-output copies on a stream of
+    // their own ("copy_stream").  ex1 1080p, host outputs, one MI355X, ms/frame: 3 slots 1.83; 2 slots
+    // + copy stream 1.83; 3 slots + MT stream 1.82; 2 slots 2.20; 2 slots + MT stream 2.00.  The
+    // default keeps three streams (HIP's default of four hardware queues per process, so no stream
+    // shares a queue)
+    int nslots = 3;
+    bool use_mt_stream = false;
+    bool use_copy_stream = false;
     FrameSlot* f = &slots[0];
     bool pipeline = false;  // option "pipeline": size every slot on every frame (no first-use allocation)
     int next_slot = 0;      // slot of the next asynchronous frame
@@ -1203,6 +1066,11 @@ struct srt_ctx {
     srt_mt_state* mt_chain = nullptr;
     int mt_pos = 0;
     hipEvent_t mt_done = nullptr;  // recorded after the last frame's stream generation
+    int mt_cur = 0;                // which of the two final-window buffers is current (mt_dump)
+    // single-pass frames generate their numpy stream on a stream of their own, so the generation of
+    // frame k+1 runs beside frame k's trace (their order is this stream's order)
+    hipStream_t mt_stream = nullptr;
+    hipStream_t copy_stream = nullptr;  // option copy_stream: the host-output copies of pipelined frames
     bool mt_tables = false;
     // multi-GPU (srt_comm_init / srt_comm_init_all)
     ncclComm_t comm = nullptr;
@@ -1395,35 +1263,36 @@ namespace {
 
 // ---- numpy's stream on the device (rt_mt.h): scratch c->mt = jump tables | key 0 | key 1 | dump ----
 constexpr int64_t MT_NTAB = rtmt::TABLE_WORDS;
-constexpr size_t MT_LDS_BYTES = (size_t)(MT_YBLOCKS + 1) * rtmt::N * 4;
 uint32_t* mt_key0(srt_ctx* c) { return c->mt + MT_NTAB; }
-uint32_t* mt_dump(srt_ctx* c) { return c->mt + MT_NTAB + 2 * rtmt::N; }
+// the final window of the last queued generation (two alternate, so the next frame's generation
+// reads the previous one in place while writing its own)
+uint32_t* mt_dump(srt_ctx* c) { return c->mt + MT_NTAB + (2 + c->mt_cur) * rtmt::N; }
 
 int mt_ensure(srt_ctx* c) {
     if (c->mt) return SRT_OK;
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_round),
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_jump),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)MT_LDS_BYTES));
-    HIP_TRY(dalloc(&c->mt, MT_NTAB + 3 * rtmt::N));
+    HIP_TRY(dalloc(&c->mt, MT_NTAB + 4 * rtmt::N + (int64_t)rtmt::SEGS * rtmt::N));
     HIP_TRY(hipMemcpy(c->mt, rtmt::tables_flat(), MT_NTAB * 4, hipMemcpyHostToDevice));
     return SRT_OK;
 }
 
-// Queue on `st`: from the key window in mt_key0 at position `pos`, n_out doubles into `out` (device)
-// and n_skip more draws; the window holding the last consumed word goes to mt_dump.  Returns the
+// Queue on `st`: from the key window `key` (device) at position `pos`, n_out doubles into `out`
+// (device) and n_skip more draws; the window holding the last consumed word becomes mt_dump(c).  Returns the
 // numpy position of that window in *final_pos.  `plane` > 0: only the doubles of the planes
 // (index % 4) in `plane_mask` are stored (a pinhole camera reads no lens-disk pair).
-int mt_launch(srt_ctx* c, hipStream_t st, int pos, int64_t n_out, int64_t n_skip, double* out, int* final_pos,
+int mt_launch(srt_ctx* c, hipStream_t st, const uint32_t* key, int pos, int64_t n_out, int64_t n_skip, double* out, int* final_pos,
               int64_t plane = 0, int plane_mask = 15) {
     uint32_t* keys[2] = {c->mt + MT_NTAB, c->mt + MT_NTAB + rtmt::N};
     const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
     for (size_t r = 0; r < plan.rounds.size(); ++r) {
         const rtmt::Round& R = plan.rounds[r];
         MtArgs A{};
-        A.key = keys[r & 1];
+        A.key = r == 0 ? key : keys[r & 1];
         A.tab = c->mt;
         A.out = out;
         A.chain_dst = R.chain ? keys[(r + 1) & 1] : nullptr;
-        A.dump_dst = R.dump_at >= 0 ? mt_dump(c) : nullptr;
+        A.dump_dst = R.dump_at >= 0 ? c->mt + MT_NTAB + (2 + (c->mt_cur ^ 1)) * rtmt::N : nullptr;
         A.words = R.words;
         A.double_base = R.double_base;
         A.n_out = n_out;
@@ -1432,9 +1301,16 @@ int mt_launch(srt_ctx* c, hipStream_t st, int pos, int64_t n_out, int64_t n_skip
         // the block's doubles span at most two planes when a plane holds >= 312 of them
         A.plane = plane >= 1024 ? plane : 0;
         A.plane_mask = plane_mask;
-        hipLaunchKernelGGL(k_mt_round, dim3(R.nseg), dim3(MT_THREADS), MT_LDS_BYTES, st, A);
+        // segment windows (table after the keys and final windows), then the generators
+        uint32_t* win = c->mt + MT_NTAB + 4 * rtmt::N;
+        if (R.nseg > 1) {
+            hipLaunchKernelGGL(k_mt_jump, dim3(R.nseg - 1), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
+            HIP_TRY(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, A, (const uint32_t*)win);
         HIP_TRY(hipGetLastError());
     }
+    c->mt_cur ^= 1;
     *final_pos = plan.final_pos;
     return SRT_OK;
 }
@@ -1505,9 +1381,10 @@ void clear_host_flags(srt_ctx* c, const FramePlan& F) {
 int ensure_slot(FrameSlot& f) {
     if (f.stream) return SRT_OK;
     HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&f.copy_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&f.jit_ready, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f.resolved, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f.copied, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&f.jit_free, hipEventDisableTiming));
     HIP_TRY(dalloc(&f.counts, SRT_MAX_DEPTHS * NSHARD));
     HIP_TRY(dalloc(&f.flags, 2));
     HIP_TRY(dalloc(&f.shadow, NSHARD));
@@ -1518,7 +1395,6 @@ int ensure_slot(FrameSlot& f) {
 void free_slot(FrameSlot& f) {
     if (!f.stream) return;
     (void)hipStreamSynchronize(f.stream);
-    (void)hipStreamSynchronize(f.copy_stream);
     free_list(f.queue_bufs);
     free_list(f.ring_bufs);
     void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb};
@@ -1526,9 +1402,10 @@ void free_slot(FrameSlot& f) {
         if (p) (void)hipFree(p);
     for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     if (f.host) (void)hipHostFree(f.host);
+    (void)hipEventDestroy(f.jit_ready);
     (void)hipEventDestroy(f.resolved);
     (void)hipEventDestroy(f.copied);
-    (void)hipStreamDestroy(f.copy_stream);
+    (void)hipEventDestroy(f.jit_free);
     (void)hipStreamDestroy(f.stream);
     f = FrameSlot{};
 }
@@ -1545,9 +1422,9 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     for (FrameSlot& f : c->slots)
         if (f.stream) {
             HIP_TRY(hipStreamSynchronize(f.stream));
-            HIP_TRY(hipStreamSynchronize(f.copy_stream));
             f.copy_pending = false;
         }
+    if (c->copy_stream) HIP_TRY(hipStreamSynchronize(c->copy_stream));
     c->async_pending = 0;
     if (c->mt_chain) {  // numpy's state after the last asynchronous frame's draws
         HIP_TRY(hipMemcpy(c->mt_chain->key, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost));
@@ -1557,8 +1434,8 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     int first_err = SRT_OK;
     bool overflow = false;
     srt_stats last{};
-    for (int k = 0; k < FRAME_SLOTS; ++k) {
-        FrameSlot& f = c->slots[(c->last_slot + 1 + k) % FRAME_SLOTS];  // the last frame's slot last
+    for (int k = 0; k < MAX_FRAME_SLOTS; ++k) {
+        FrameSlot& f = c->slots[(c->last_slot + 1 + k) % MAX_FRAME_SLOTS];  // the last frame's slot last
         if (!f.pending) continue;
         c->f = &f;
         srt_stats S{};
@@ -1691,6 +1568,8 @@ int srt_destroy(srt_ctx* c) {
     free_list(c->scene_bufs);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->mt_done) (void)hipEventDestroy(c->mt_done);
+    if (c->mt_stream) (void)hipStreamDestroy(c->mt_stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -1707,6 +1586,21 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
+    if (!strcmp(key, "slots") || !strcmp(key, "mt_stream") || !strcmp(key, "copy_stream")) {
+        if (!strcmp(key, "slots") && (value < 1 || value > MAX_FRAME_SLOTS)) return fail(SRT_ERR_ARG, "slots: 1..4");
+        HIP_TRY(hipSetDevice(c->device));
+        int rc = finish_async(c, nullptr);  // the frames in flight finish on the old arrangement
+        if (rc) return rc;
+        if (!strcmp(key, "slots")) {
+            c->nslots = (int)value;
+            c->next_slot = 0;
+        } else if (!strcmp(key, "mt_stream")) {
+            c->use_mt_stream = value != 0;
+        } else {
+            c->use_copy_stream = value != 0;
+        }
+        return SRT_OK;
+    }
     return fail(SRT_ERR_ARG, std::string("unknown option ") + key);
 }
 
@@ -2003,18 +1897,23 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     };
     if ((rc = ensure_frame(*c->f))) return rc;
     if (async || c->pipeline) {
-        for (FrameSlot& other : c->slots)
+        for (int k = 0; k < c->nslots; ++k) {
+            FrameSlot& other = c->slots[k];
             if (&other != c->f && other.pending == 0) {
                 if ((rc = ensure_slot(other))) return rc;
                 if ((rc = ensure_frame(other))) return rc;
             }
+        }
     }
     if (use_mt && !c->mt_done) HIP_TRY(hipEventCreateWithFlags(&c->mt_done, hipEventDisableTiming));
     const Variant& V = pick_variant(c->mats);
-    // resolve targets: outputs already in device memory are written in place by k_resolve (no copies);
-    // a shard resolves into its slot tiles (gathered afterwards)
-    double* res_rgb = sharded ? (gather_rgb ? c->f->rgb : nullptr) : a->out_rgb ? (rgb_dev ? a->out_rgb : c->f->rgb) : nullptr;
-    uint8_t* res_u8 = sharded ? c->f->u8 : a->out_srgb8 ? (u8_dev ? a->out_srgb8 : c->f->u8) : nullptr;
+    // resolve targets: outputs in device memory are written in place by the resolve; host outputs
+    // are resolved into the slot buffers and copied by DMA on the frame's stream (57 GB/s measured
+    // for the ex1 1080p RGB, against 28 GB/s for a resolve kernel storing straight into pinned
+    // memory over PCIe); a shard resolves into its slot tiles (gathered afterwards)
+    const bool rgb_direct = rk == 1, u8_direct = uk == 1;
+    double* res_rgb = sharded ? (gather_rgb ? c->f->rgb : nullptr) : a->out_rgb ? (rgb_direct ? a->out_rgb : c->f->rgb) : nullptr;
+    uint8_t* res_u8 = sharded ? c->f->u8 : a->out_srgb8 ? (u8_direct ? a->out_srgb8 : c->f->u8) : nullptr;
     // only the depths this frame can reach are handed back and cleared per pass
     const int64_t used_words = std::min<int64_t>(F.cnt_words, (int64_t)(F.dcap + 2) * NSHARD);
     // the numpy stream continues on the device from the previous asynchronous frame (same `mt`)
@@ -2029,16 +1928,25 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         }
         c->f->dirty = true;
         int mt_pos = 0;
+        const uint32_t* mt_key = nullptr;
+        // the stream the numpy-stream generation runs on: the MT stream for a single-pass frame
+        // (it waits until the slot's previous frame has read its jitter), else the frame's stream
+        hipStream_t mst = c->f->stream;
         if (use_mt) {
+            if (F.npass == 1 && c->use_mt_stream) {
+                if (!c->mt_stream) HIP_TRY(hipStreamCreateWithFlags(&c->mt_stream, hipStreamNonBlocking));
+                mst = c->mt_stream;
+                if (c->f->jit_busy) HIP_TRY(hipStreamWaitEvent(mst, c->f->jit_free, 0));
+            }
             // this frame's stream starts where the previous frame's ended (device dump window) or at
             // the caller's state
+            if (c->mt_done) HIP_TRY(hipStreamWaitEvent(mst, c->mt_done, 0));
             if (mt_chained) {
-                HIP_TRY(hipStreamWaitEvent(c->f->stream, c->mt_done, 0));
-                HIP_TRY(hipMemcpyAsync(mt_key0(c), mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToDevice, c->f->stream));
+                mt_key = mt_dump(c);
                 mt_pos = c->mt_pos;
             } else {
-                if (c->mt_done) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->mt_done, 0));
-                HIP_TRY(hipMemcpyAsync(mt_key0(c), a->mt->key, rtmt::N * 4, hipMemcpyHostToDevice, c->f->stream));
+                HIP_TRY(hipMemcpyAsync(mt_key0(c), a->mt->key, rtmt::N * 4, hipMemcpyHostToDevice, mst));
+                mt_key = mt_key0(c);
                 mt_pos = a->mt->pos;
             }
         }
@@ -2073,14 +1981,17 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 // pass); a shard reads its rows by global pixel
                 const int64_t n_out = (int64_t)ns * 4 * W * Hf;
                 const int64_t n_skip = (p + 1 == F.npass) ? 4 * W * Hf : 0;
-                if (p > 0)
-                    HIP_TRY(hipMemcpyAsync(mt_key0(c), mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToDevice, c->f->stream));
+                if (p > 0) mt_key = mt_dump(c);  // the previous pass's final window
                 // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
-                if ((rc = mt_launch(c, c->f->stream, mt_pos, n_out, n_skip, c->f->jit, &mt_pos, W * Hf,
+                if ((rc = mt_launch(c, mst, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos, W * Hf,
                                     cam->lens_radius != 0.0 ? 15 : 3)))
                     return rc;
                 // the next frame's stream may start as soon as this one's is generated
-                if (p + 1 == F.npass) HIP_TRY(hipEventRecord(c->mt_done, c->f->stream));
+                if (p + 1 == F.npass) HIP_TRY(hipEventRecord(c->mt_done, mst));
+                if (mst != c->f->stream) {
+                    HIP_TRY(hipEventRecord(c->f->jit_ready, mst));
+                    HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->jit_ready, 0));
+                }
                 P.jitter = c->f->jit;
                 P.jit_plane = W * Hf;
                 P.jit_global = 1;
@@ -2115,6 +2026,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 HIP_TRY(hipGetLastError());
                 HIP_TRY(hipEventRecord(ev[1], c->f->stream));
                 HIP_TRY(hipEventRecord(ev[F.dcap + 1], c->f->stream));
+                if (mst != c->f->stream) {  // the next generation into this slot may start
+                    HIP_TRY(hipEventRecord(c->f->jit_free, c->f->stream));
+                    c->f->jit_busy = true;
+                }
             } else {
             // depth 0: raygen fused with the trace step
             P.depth = 0;
@@ -2126,6 +2041,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                                dim3(BLOCK), lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
+            if (mst != c->f->stream) {  // the next generation into this slot may start
+                HIP_TRY(hipEventRecord(c->f->jit_free, c->f->stream));
+                c->f->jit_busy = true;
+            }
             P.fb_first = 0;
             for (int d = 1; d <= F.dcap; ++d) {
                 if (F.chain_from > 0 && d > F.chain_from) break;  // traced by the chain kernel
@@ -2187,31 +2106,36 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (async) {
             // (a synchronous frame gathers after its retries: every rank gathers each frame once)
             if (sharded && !c->defer_gather && (rc = gather_frame(c))) return rc;
+            if (!sharded && ((a->out_srgb8 && !u8_direct) || (a->out_rgb && !rgb_direct))) {
+                hipStream_t cs = c->f->stream;
+                if (c->use_copy_stream) {
+                    if (!c->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+                    cs = c->copy_stream;
+                    HIP_TRY(hipEventRecord(c->f->resolved, c->f->stream));
+                    HIP_TRY(hipStreamWaitEvent(cs, c->f->resolved, 0));
+                }
+                if (a->out_srgb8 && !u8_direct)
+                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, cs));
+                if (a->out_rgb && !rgb_direct)
+                    HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, cs));
+                if (c->use_copy_stream) {
+                    HIP_TRY(hipEventRecord(c->f->copied, cs));
+                    c->f->copy_pending = true;
+                }
+            }
             // host outputs (pinned) are copied on the frame's stream; stats and errors come with
             // srt_render_finish; the next asynchronous frame goes to the next slot
-            if (!sharded && ((a->out_rgb && !rgb_dev) || (a->out_srgb8 && !u8_dev))) {
-                HIP_TRY(hipEventRecord(c->f->resolved, c->f->stream));
-                HIP_TRY(hipStreamWaitEvent(c->f->copy_stream, c->f->resolved, 0));
-                if (a->out_srgb8 && !u8_dev)
-                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost,
-                                           c->f->copy_stream));
-                if (a->out_rgb && !rgb_dev)
-                    HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost,
-                                           c->f->copy_stream));
-                HIP_TRY(hipEventRecord(c->f->copied, c->f->copy_stream));
-                c->f->copy_pending = true;
-            }
             if (use_mt) c->mt_chain = a->mt;
             c->async_pending++;
             c->f->pending++;
             c->f->plan = F;
             c->last_slot = (int)(c->f - c->slots);
-            c->next_slot = (c->last_slot + 1) % FRAME_SLOTS;
+            c->next_slot = (c->last_slot + 1) % c->nslots;
             return SRT_OK;
         }
-        if (!sharded && a->out_rgb && !rgb_dev)
+        if (!sharded && a->out_rgb && !rgb_direct)
             HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->f->stream));
-        if (!sharded && a->out_srgb8 && !u8_dev)
+        if (!sharded && a->out_srgb8 && !u8_direct)
             HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->f->stream));
         c->f->dirty = true;
         HIP_TRY(hipStreamSynchronize(c->f->stream));
@@ -2470,7 +2394,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     hipStream_t st = c->f->stream;
     HIP_TRY(hipMemcpyAsync(mt_key0(c), key, rtmt::N * 4, hipMemcpyHostToDevice, st));
     int final_pos = 0;
-    if ((rc = mt_launch(c, st, pos, n_out, n_skip, dst, &final_pos))) return rc;
+    if ((rc = mt_launch(c, st, mt_key0(c), pos, n_out, n_skip, dst, &final_pos))) return rc;
     if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(key_out, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2641,6 +2565,7 @@ int srt_synchronize(srt_ctx* c) {
     HIP_TRY(hipSetDevice(c->device));
     for (FrameSlot& f : c->slots)
         if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
+    if (c->copy_stream) HIP_TRY(hipStreamSynchronize(c->copy_stream));
     return SRT_OK;
 }
 

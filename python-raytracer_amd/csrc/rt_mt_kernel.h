@@ -1,0 +1,258 @@
+// rt_mt_kernel.h -- the device generator of numpy's legacy `np.random.rand` stream (rt_mt.h):
+// k_mt_round, one workgroup per 2^19-word segment of a round.  Included by rt_kernels.hip (the
+// library) and tools/mt_bench.hip (a stand-alone timing harness for this kernel).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <climits>
+
+#include "rt_mt.h"
+
+namespace rtmt_dev {
+
+struct MtArgs {
+    const uint32_t* key;   // the round's key window (624 words)
+    const uint32_t* tab;   // jump polynomials x^(sL-1), s = 1..SEGS-1 (624 words each)
+    double* out;           // doubles of the whole call
+    uint32_t* chain_dst;   // next round's key window (written by segment SEGS-1) or null
+    uint32_t* dump_dst;    // final numpy key window or null
+    int64_t words;         // words consumed by this round
+    int64_t double_base;   // first double of this round
+    int64_t n_out;         // doubles to write (the rest are skipped draws)
+    int64_t dump_at;       // round-relative start of the final state window, or -1
+    int64_t plane;         // doubles per jitter plane (0: write every double)
+    int32_t plane_mask;    // bit k set: write the doubles of planes with index % 4 == k
+    int32_t pos;           // outputs start at word `pos` of the key window
+};
+
+// Two launches per round.
+//  k_mt_jump: one workgroup per segment s >= 1 that has anything to store.  y = the 34 x 624 raw words
+//    generated from the key window (LDS), then W'[m] = XOR_{i : p_i} y[i + m] -- wave v takes
+//    coefficient words [78 v, 78 v + 78), lane g the ten outputs m = 10 g .. 10 g + 9 with
+//    y[32 w + 10 g .. + 41] in registers, so a set bit costs ten register XORs and no LDS traffic; the
+//    eight waves' partial windows are XOR-reduced through LDS and written to the window table.
+//  k_mt_gen: MT_GEN_THREADS per segment.  A ring of three 624-word blocks in LDS; the next block is
+//    made in three dependent stages of 227 / 227 / 170 words (x_{k+624} = x_{k+397} ^ twist(x_k,
+//    x_{k+1}): stage two and three take their x_{k+397} from the thread's own earlier word) while the
+//    current block's 312 doubles are tempered and stored.  7.5 KB of LDS and five waves per segment:
+//    the trace kernels of the previous frame keep the rest of the CU.
+constexpr int MT_THREADS = 512;
+constexpr int MT_WAVES = MT_THREADS / 64;
+constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 78 coefficient words
+constexpr int MT_G = 10;                              // window outputs per lane in the jump
+constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
+constexpr int MT_RED = 640;                           // per-wave stride of the reduction buffer
+static_assert(MT_CW_PER_WAVE * MT_WAVES == rtmt::N, "coefficient words split evenly over the waves");
+static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 42 <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
+static_assert(MT_WAVES * MT_RED <= MT_YBLOCKS * rtmt::N, "the reduction aliases y");
+constexpr size_t MT_LDS_BYTES = (size_t)(MT_YBLOCKS + 1) * rtmt::N * 4;  // y + coefficient words
+// generator threads per segment: 5 waves (227 make the next block, 312 store the current one).
+// Measured (222 segments, ex1 1080p pinhole planes): 1 wave 1.17 ms, 4 waves 0.64, 5 waves 0.50,
+// 8 waves 0.50 -- one wave is VALU-issue bound (~3000 cycles per 624-word block)
+constexpr int MT_GEN_THREADS = 320;
+
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic, not for its global
+// stores (__syncthreads() would also drain the output stores)
+__device__ __forceinline__ void mt_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+    __builtin_amdgcn_s_barrier();
+}
+
+// block n (624 words) from block p by a workgroup.  Thread t < 227 makes words t, 227 + t and 454 + t:
+// each needs only block p and the thread's own earlier word, so no barrier is needed inside the
+// block; word 623 also needs word 0 of block n, which thread 169 recomputes.
+__device__ __forceinline__ void mt_next_block(const uint32_t* p, uint32_t* n, int t) {
+    if (t < 227) {
+        const uint32_t a0 = p[t], a1 = p[t + 1], a2 = p[t + 397], b0 = p[227 + t], b1 = p[228 + t];
+        const uint32_t c0 = t < 170 ? p[454 + t] : 0u;
+        uint32_t c1 = t < 169 ? p[455 + t] : 0u;
+        const uint32_t wa = rtmt::next_word(a0, a1, a2);
+        const uint32_t wb = rtmt::next_word(b0, b1, wa);
+        n[t] = wa;
+        n[227 + t] = wb;
+        if (t == 169) c1 = rtmt::next_word(p[0], p[1], p[397]);  // word 0 of block n
+        if (t < 170) n[454 + t] = rtmt::next_word(c0, c1, wb);
+    }
+}
+
+// What segment s of a round stores and generates (uniform over the segment's threads).
+struct MtSeg {
+    int64_t ws;       // round-relative index of the segment's window
+    int64_t lo;       // first output word
+    int64_t dbase;    // double of pair 0
+    int64_t gen_end;  // words to generate (exclusive)
+    int64_t chain_at;
+    int kend;         // pairs [0, kend) are stored (minus the planes outside plane_mask)
+    bool chain, dump;
+    __device__ bool idle() const { return kend == 0 && !chain && !dump; }
+};
+
+__device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
+    MtSeg g;
+    g.ws = rtmt::window_start(s);
+    const int64_t end = A.pos + A.words;  // round-relative, exclusive
+    g.lo = (int64_t)s * rtmt::L + A.pos;
+    const int64_t hi = min((int64_t)(s + 1) * rtmt::L + A.pos, end);
+    const int64_t npairs = hi > g.lo ? (hi - g.lo) / 2 : 0;
+    g.dbase = A.double_base + (g.lo - A.pos) / 2;
+    // a skipped draw (beyond n_out, or in a plane outside plane_mask) is only stepped over
+    const int kmax = (int)max<int64_t>(0, min<int64_t>(npairs, A.n_out - g.dbase));
+    g.kend = kmax;
+    if (A.plane > 0 && kmax > 0) {
+        g.kend = 0;
+        for (int64_t pi = g.dbase / A.plane; pi * A.plane < g.dbase + kmax; ++pi)
+            if ((A.plane_mask >> (pi & 3)) & 1) g.kend = (int)min<int64_t>(kmax, (pi + 1) * A.plane - g.dbase);
+    }
+    g.gen_end = g.lo + 2 * (int64_t)g.kend;
+    g.chain = A.chain_dst && s == rtmt::SEGS - 1;
+    g.chain_at = rtmt::window_start(rtmt::SEGS);
+    if (g.chain) g.gen_end = max(g.gen_end, g.chain_at + rtmt::N);
+    g.dump = A.dump_dst && rtmt::dumps(s, A.dump_at);
+    if (g.dump) g.gen_end = max(g.gen_end, A.dump_at + rtmt::N);
+    return g;
+}
+
+// block s - 1 of the grid: the window of segment s >= 1 into win + 624 s
+__global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win) {
+    extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words (+ 624 coefficient words)
+    uint32_t* y = mt_lds;
+    uint32_t* coef = mt_lds + MT_YBLOCKS * rtmt::N;
+    uint32_t* red = mt_lds;  // MT_WAVES x MT_RED (aliases y once it is read)
+    const int s = blockIdx.x + 1;
+    const int t = threadIdx.x;
+    if (mt_seg(A, s).idle()) return;
+    const uint32_t* poly = A.tab + (int64_t)(s - 1) * rtmt::N;
+    for (int m = t; m < rtmt::N; m += MT_THREADS) {
+        y[m] = A.key[m];
+        coef[m] = poly[m];
+    }
+    __syncthreads();
+    for (int q = 0; q + 1 < MT_YBLOCKS; ++q) {
+        mt_next_block(y + q * rtmt::N, y + (q + 1) * rtmt::N, t);
+        mt_barrier();
+    }
+    const int wv = t >> 6, g = t & 63;
+    uint32_t acc[MT_G];
+#pragma unroll
+    for (int k = 0; k < MT_G; ++k) acc[k] = 0u;
+    for (int cw_i = wv * MT_CW_PER_WAVE; cw_i < (wv + 1) * MT_CW_PER_WAVE; ++cw_i) {
+        const uint32_t cw = __builtin_amdgcn_readfirstlane(coef[cw_i]);
+        if (cw == 0u) continue;
+        // y[32 cw_i + 10 g ...]: an even word index, so 8-byte aligned pair loads
+        const uint2* yp = reinterpret_cast<const uint2*>(y + 32 * cw_i + MT_G * g);
+        uint32_t r[32 + MT_G];
+#pragma unroll
+        for (int k = 0; k < (32 + MT_G) / 2; ++k) {
+            const uint2 v = yp[k];
+            r[2 * k] = v.x;
+            r[2 * k + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            if (cw & (1u << j)) {  // wave-uniform
+#pragma unroll
+                for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + k];
+            }
+        }
+    }
+    __syncthreads();  // every wave is done reading y
+#pragma unroll
+    for (int k = 0; k < MT_G; ++k) red[wv * MT_RED + MT_G * g + k] = acc[k];
+    __syncthreads();
+    for (int m = t; m < rtmt::N; m += MT_THREADS) {
+        uint32_t w = 0u;
+#pragma unroll
+        for (int v = 0; v < MT_WAVES; ++v) w ^= red[v * MT_RED + m];
+        win[(int64_t)s * rtmt::N + m] = w;
+    }
+}
+
+// NT threads per segment: generate from its window (the key for segment 0) and store its doubles.
+// NT = 64: one wave (no workgroup barrier, the next block in three staged chunks); NT >= 256: the
+// workgroup form (threads < 227 make three words each)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
+    __shared__ uint32_t ring[3 * rtmt::N];
+    const int s = blockIdx.x;
+    const int lane = threadIdx.x;
+    const MtSeg g = mt_seg(A, s);
+    if (g.idle()) return;
+    const uint32_t* w0p = s == 0 ? A.key : win + (int64_t)s * rtmt::N;
+    for (int m = lane; m < rtmt::N; m += NT) ring[m] = w0p[m];
+    __syncthreads();
+    // block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it holds
+    const int off0 = (int)(g.lo - g.ws);  // 1 .. 625 (s > 0) or pos (s == 0)
+    const int c0 = -((off0 + 1) >> 1);    // pair index of block 0's first pair
+    double* outp = A.out + g.dbase;
+    // plane of pair k: pidx while k < kb, then pidx + 1 (a block's 312 pairs span at most two planes)
+    int64_t pidx = 0, kb = INT64_MAX;
+    if (A.plane > 0) {
+        pidx = g.dbase / A.plane;
+        kb = (pidx + 1) * A.plane - g.dbase;
+    }
+    int kq = c0;  // pair of block q's first thread slot
+    int slot = 0, prev = 2, next = 1;
+    for (int64_t b0 = g.ws; b0 < g.gen_end; b0 += rtmt::N) {
+        const uint32_t* p = ring + slot * rtmt::N;
+        uint32_t* n = ring + next * rtmt::N;
+        if (NT >= 256) {
+            if (b0 + rtmt::N < g.gen_end) mt_next_block(p, n, lane);
+        } else if (b0 + rtmt::N < g.gen_end) {
+            // stage 1: words j < 227; stage 2: 227 + j; stage 3: 454 + j (j < 170), chunk c = lane + 64 c
+            uint32_t wa[4], wb[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int j = lane + 64 * c;
+                const int jj = j < 227 ? j : 226;
+                wa[c] = rtmt::next_word(p[jj], p[jj + 1], p[jj + 397]);
+                wb[c] = rtmt::next_word(p[227 + jj], p[228 + jj], wa[c]);
+            }
+            const uint32_t n0 = __shfl(wa[0], 0);  // word 0 of block n (for word 623)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int j = lane + 64 * c;
+                if (j < 227) {
+                    n[j] = wa[c];
+                    n[227 + j] = wb[c];
+                }
+                if (j < 170) n[454 + j] = rtmt::next_word(p[454 + j], j == 169 ? n0 : p[min(455 + j, 623)], wb[c]);
+            }
+        }
+        if (kq >= kb) {
+            ++pidx;
+            kb += A.plane;
+        }
+        const uint32_t* cur = p;
+#pragma unroll
+        for (int i = 0; i < (312 + NT - 1) / NT; ++i) {
+            const int t = lane + NT * i;
+            const int k = kq + t;
+            if (t < 312 && k >= 0 && k < g.kend &&
+                (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1))) {
+                const int o = off0 + 2 * (c0 + t);  // in-block offset of the pair's first word: -1 .. 622
+                const uint32_t x0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
+                const uint32_t x1 = cur[o + 1];
+                outp[k] = rtmt::to_double(rtmt::temper(x0), rtmt::temper(x1));
+            }
+        }
+        if (g.chain || g.dump) {
+            for (int m = lane; m < rtmt::N; m += NT) {
+                const int64_t x = b0 + m;
+                const uint32_t v = cur[m];
+                if (g.chain && x >= g.chain_at && x < g.chain_at + rtmt::N) A.chain_dst[x - g.chain_at] = v;
+                if (g.dump && x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = v;
+            }
+        }
+        kq += 312;
+        prev = slot;
+        slot = next;
+        next = next == 2 ? 0 : next + 1;
+        if (NT == 64)
+            __syncthreads();  // one wave: orders the block's LDS writes before the next block's reads
+        else
+            mt_barrier();
+    }
+}
+
+}  // namespace rtmt_dev
