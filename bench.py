@@ -53,16 +53,17 @@ CONFIGS = {
 }
 
 RAY_BYTES = 84  # one queued ray record (rt_kernels.hip Queue): O, D, throughput f64 x 9 + 3 u32
+BYTES_MODEL = {
+    "primary": "jitter read (2 f64 per sample, 4 for a thin lens) + the depth-1 children written to the queue "
+               "(84 B each) + the framebuffer store (3 f64 per pixel); depth-0 rays live in registers",
+    "frame": "jitter read + every secondary ray written to and read back from its wave's ring (2 x 84 B) + the "
+             "fused resolve's uint8 and linear-RGB stores (27 B per pixel)",
+}
 
 
 def kernel_bytes_model(stats, spp, npix, lens):
     """Algorithmic HBM bytes of one launch of the dominant kernel, from what it moves (DESIGN.md §3);
-    texture and scene-table reads are cache-resident and not counted.
-      k_primary (wavefront path): depth-0 rays are generated and shaded in registers, so jitter read
-        (2 f64 per sample, 4 for a thin lens) + the depth-1 children written to the queue (84 B) +
-        the framebuffer store (3 f64 per pixel);
-      k_frame (branching scenes, one pass): jitter read + every secondary ray written to and read
-        back from its wave's ring (2 x 84 B) + the fused resolve's uint8 and linear-RGB stores."""
+    texture and scene-table reads are cache-resident and not counted (BYTES_MODEL)."""
     planes = 4 if lens else 2
     rpd = stats["rays_per_depth"]
     if stats["kernel_path"] == "frame":
@@ -160,18 +161,60 @@ def cpu_baseline(builder, W, H, depth, spp, budget_s=15.0):
     return one
 
 
-def pmc_traffic(config, kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary of this config
-    (profiles/rNN_traffic_<config>.json, tools/pmc_traffic.py: separate rocprofv3 --pmc passes of
-    FETCH_SIZE (x2 on gfx950) and WRITE_SIZE of this bench), or None."""
-    files = sorted(ROOT.glob("profiles/r*_traffic_%s.json" % config))
+def pmc_counters(config, kernel):
+    """Per-launch counters of `kernel` from the newest committed PMC summary of this config
+    (profiles/rNN_counters_<config>.json, tools/pmc_summary.py over separate rocprofv3 --pmc passes of
+    this bench: FETCH_SIZE, WRITE_SIZE, SQ fp64/VALU/wait counters), or (None, None)."""
+    files = sorted(ROOT.glob("profiles/r*_counters_%s.json" % config))
     if not files:
-        return None, None, None
+        return None, None
     rec = json.loads(files[-1].read_text())
     for name, k in rec["kernels"].items():
-        if kernel in name and "traffic_bytes" in k:
-            return k["traffic_bytes"] / 1e9, files[-1].name, k
-    return None, None, None
+        if kernel in name:
+            return k, files[-1].name
+    return None, None
+
+
+def roofline(kname, kms, model_bytes, frame_path, krec, src):
+    """The dominant kernel against the MI355X roofline.  achieved = algorithmic bytes / launch time
+    (HIP events); traffic = PMC HBM bytes per launch; the arithmetic intensity (counted fp64 FLOP per
+    PMC byte) against the ridge (78.6 TF / 8 TB/s) classifies the bound; the counters then say what
+    holds the kernel below that roof."""
+    sec = kms * 1e-3
+    roof = {"kernel": kname, "kernel_ms": round(kms, 4), "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "achieved": round(model_bytes / sec / 1e9, 2), "frac": round(model_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_GB_per_launch": round(model_bytes / 1e9, 4),
+            "bytes_model": BYTES_MODEL["frame" if frame_path else "primary"], "traffic": None}
+    if krec is None or "traffic_bytes" not in krec:
+        return roof
+    tb = krec["traffic_bytes"]
+    roof["traffic"] = round(tb / 1e9, 4)
+    roof["traffic_unit"] = "GB per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)"
+    roof["traffic_frac"] = round(tb / sec / 1e9 / HBM_PEAK_GBS, 4)
+    roof["model_over_traffic"] = round(model_bytes / tb, 3)
+    roof["source"] = src
+    c = krec.get("counters", {})
+    if krec.get("fp64_flop"):
+        ai = krec["fp64_flop"] / tb
+        ridge = FP64_PEAK_TFS * 1e3 / HBM_PEAK_GBS
+        tf = krec["fp64_flop"] / sec / 1e12
+        roof["bound"] = "hbm" if ai < ridge else "fp64-valu"
+        roof["arith_intensity_flop_per_byte"] = round(ai, 2)
+        roof["ridge_flop_per_byte"] = round(ridge, 2)
+        roof["fp64"] = {"achieved_TFLOPs": round(tf, 3), "peak": FP64_PEAK_TFS, "frac": round(tf / FP64_PEAK_TFS, 4),
+                        "note": "64 x (ADD + MUL + TRANS + 2 FMA) f64 wave instructions: counts masked lanes"}
+    if "SQ_INSTS_VALU" in c and "SQ_INSTS_VALU_FMA_F64" in c:
+        f64 = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_FMA_F64"]
+        cycles = 4 * f64 + 2 * (c["SQ_INSTS_VALU"] - f64)  # wave64 on SIMD32: 2 cycles, f64 at half rate: 4
+        roof["valu_issue_frac"] = round(cycles / (1024 * sec * 2.4e9), 4)
+    if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
+        roof["wave_wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+    if "valu_issue_frac" in roof and "wave_wait_frac" in roof:
+        roof["limiter"] = ("latency: 2 waves/SIMD (register-bound); waves wait on memory %.0f%% of their cycles, VALU "
+                           "issue %.0f%% busy, HBM %.0f%% of peak" % (100 * roof["wave_wait_frac"],
+                                                                    100 * roof["valu_issue_frac"],
+                                                                    100 * roof["traffic_frac"]))
+    return roof
 
 
 def comm_id_exchange(lib, N, rank, world):
@@ -199,8 +242,8 @@ def comm_id_exchange(lib, N, rank, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
     ap.add_argument("--rng", default="mt", choices=["mt", "device"],
                     help="mt: the reference's numpy stream generated on the GPU inside every step; device: Philox")
@@ -388,27 +431,22 @@ def main():
             st0 = sec["stats"]
             frame_path = st0[0]["kernel_path"] == "frame"
             kname = "k_frame" if frame_path else "k_primary"
-            kms = float(np.mean([x["ms_primary_kernel"] for x in st0]))
-            traffic, src, krec = (None, None, None) if (args.size or args.spp or world > 1 or rows32 is not None) else \
-                pmc_traffic(args.config, kname)
+            # one launch of the dominant kernel: a frame of `passes` passes launches it once per pass
+            npass = max(1, st0[0]["passes"])
+            kms = float(np.mean([x["ms_primary_kernel"] for x in st0])) / npass
+            krec, src = (None, None) if (args.size or args.spp or world > 1 or rows32 is not None) else \
+                pmc_counters(args.config, kname)
             from sightpy._shard import shard_rows
 
             npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0)) * W
-            roof = {"kernel": kname, "kernel_ms": round(kms, 4), "unit": "GB/s", "peak": HBM_PEAK_GBS}
-            if st0[0]["passes"] == 1:
-                model = kernel_bytes_model(st0[0], spp, npix_rank, sc.camera.lens_radius != 0.0)
-                roof.update({"bound": "hbm", "achieved": round(model / (kms * 1e-3) / 1e9, 2),
-                             "frac": round(model / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                             "algorithmic_GB_per_launch": round(model / 1e9, 4),
-                             "bytes_model": kernel_bytes_model.__doc__.split("\n")[2 if frame_path else 1].strip()})
-            if traffic is not None:
-                roof["traffic"] = round(traffic, 4)
-                roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
-                roof["traffic_source"] = src
-                if krec and krec.get("fp64_flop") and roof.get("kernel_ms"):
-                    tf = krec["fp64_flop"] / (kms * 1e-3) / 1e12
-                    roof["compute"] = {"fp64_TFLOPs": round(tf, 3), "peak": FP64_PEAK_TFS,
-                                       "frac": round(tf / FP64_PEAK_TFS, 4), "source": src}
+            st_pass = dict(st0[0])
+            st_pass["rays_per_depth"] = [r / npass for r in st0[0]["rays_per_depth"]]
+            model = kernel_bytes_model(st_pass, spp / npass, npix_rank, sc.camera.lens_radius != 0.0)
+            roof = roofline(kname, kms, model, frame_path, krec, src)
+            if npass > 1:
+                roof["passes_per_frame"] = npass
+            roof["kernel_ms_note"] = ("one launch in a synchronous frame (HIP events); pipelined frames overlap one "
+                                      "frame's tail with the next, so ms_per_step can be below it")
             rec["roofline"] = roof
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth, spp)
