@@ -217,6 +217,24 @@ def roofline(kname, kms, model_bytes, frame_path, krec, src):
     return roof
 
 
+def shared_frames(create, world, count, nbytes):
+    """`count` host frames in POSIX shared memory, named after the launcher (one node: every rank is a
+    child of one torch.distributed.run agent), as (SharedMemory, address) pairs."""
+    from multiprocessing import resource_tracker, shared_memory
+
+    out = []
+    for k in range(count):
+        name = "sightpy_%d_%s_%d" % (os.getppid(), os.environ.get("MASTER_PORT", "0"), k)
+        if create:
+            shm = shared_memory.SharedMemory(name=name, create=True, size=nbytes)
+        else:
+            shm = shared_memory.SharedMemory(name=name)
+            resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 owns (and unlinks) it
+        addr = ctypes.addressof(ctypes.c_char.from_buffer(shm.buf))
+        out.append((shm, addr))
+    return out
+
+
 def comm_id_exchange(lib, N, rank, world):
     """RCCL unique id from rank 0 to every rank through a file keyed by the launcher's pid and port
     (one node: torch.distributed.run starts every rank as a child of one agent process)."""
@@ -274,8 +292,16 @@ def main():
     sc = getattr(scenes, builder)(W, H, depth)
     lib, ctx = B.context()
     id_path = None
+    NOUT = 3  # output buffers: one per frame in flight
+    shm_frames = []
     if world > 1:
+        # the frame's linear RGB in host shared memory: every rank writes its own rows into it over
+        # its own PCIe link (SRT_RENDER_RGB_ROWS); created by rank 0 before it publishes the RCCL id
+        if rank == 0:
+            shm_frames = shared_frames(True, world, NOUT, 3 * W * H * 8)
         cid, id_path = comm_id_exchange(lib, N, rank, world)
+        if rank != 0:
+            shm_frames = shared_frames(False, world, NOUT, 3 * W * H * 8)
         N.check(lib, lib.srt_comm_init(ctx, world, rank, cid))
     N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))  # size every frame slot during the warmup
     for kv in args.option:
@@ -284,7 +310,7 @@ def main():
     B.upload(sc)
     cd = B.camera_desc(sc.camera)
     npix_full = W * H
-    flags = N.RENDER_SHARDED | N.RENDER_GATHER_RGB if world > 1 else 0
+    flags = N.RENDER_SHARDED | N.RENDER_RGB_ROWS if world > 1 else 0
     rows32 = None
     if args.shard_of > 1 and world == 1:
         from sightpy._shard import shard_rows
@@ -292,13 +318,18 @@ def main():
         rows32 = np.ascontiguousarray(shard_rows(H, args.shard_of, 0), dtype=np.int32)
         npix_full = len(rows32) * W  # the shard's outputs
 
-    # outputs: the whole frame in pinned host memory (rank 0), one pair of buffers per frame in flight
-    NOUT = 3
+    # outputs: the whole frame in pinned host memory, one pair of buffers per frame in flight (N > 1:
+    # the uint8 image on rank 0, gathered over RCCL; the linear RGB in the shared frames, every rank)
     outs = []
-    for _ in range(NOUT if rank == 0 else 0):
+    for k in range(NOUT):
         pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
-        N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full, ctypes.byref(pu)))
-        N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full * 8, ctypes.byref(pr)))
+        if rank == 0:
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full, ctypes.byref(pu)))
+        if world > 1:
+            pr = ctypes.c_void_p(shm_frames[k][1])
+            N.check(lib, lib.srt_host_register(ctx, pr, 3 * W * H * 8))
+        else:
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full * 8, ctypes.byref(pr)))
         outs.append((pu, pr))
 
     np.random.seed(0)
@@ -315,11 +346,8 @@ def main():
     frame = {"k": 0}
 
     def step(async_ok=True, st=None):
-        if outs:
-            u8, rgb = outs[frame["k"] % NOUT]
-            a.out_srgb8, a.out_rgb = u8, rgb
-        else:
-            a.out_srgb8 = a.out_rgb = None
+        u8, rgb = outs[frame["k"] % NOUT]
+        a.out_srgb8, a.out_rgb = (u8 if u8.value else None), rgb
         frame["k"] += 1
         a.flags = flags | (N.RENDER_ASYNC if async_ok else 0)
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st) if st else None))
@@ -417,7 +445,9 @@ def main():
                        "rays_per_frame": int(total_rays), "rays_per_depth_rank0": last["rays_per_depth"],
                        "shadow_rays_rank0": last["shadow_rays"], "kernel_path": last["kernel_path"],
                        "chain_from_depth": last["chain_from"],
-                       "parallelism": "row-band shards x%d, RCCL gather of uint8 + linear RGB to rank 0" % world
+                       "parallelism": "row-band shards x%d: uint8 tiles gathered to rank 0 over RCCL (xGMI); every rank "
+                                      "writes its rows of the linear RGB into the shared host frame over its own "
+                                      "PCIe link" % world
                        if world > 1 else ("diagnostic: rank 0's rows of a %d-rank job, no gather" % args.shard_of
                                           if rows32 is not None else "1 GPU"),
                        "frame": "render() entry (scene resident) -> jitter stream on the GPU -> all samples and depths "
@@ -459,8 +489,18 @@ def main():
             except OSError:
                 pass
     for pu, pr in outs:
-        lib.srt_host_free(ctx, pu)
-        lib.srt_host_free(ctx, pr)
+        if pu.value:
+            lib.srt_host_free(ctx, pu)
+        if world > 1:
+            lib.srt_host_unregister(ctx, pr)
+        else:
+            lib.srt_host_free(ctx, pr)
+    if world > 1:
+        N.check(lib, lib.srt_comm_barrier(ctx))  # every rank unregistered before rank 0 unlinks
+        for shm, _ in shm_frames:
+            shm.close()
+            if rank == 0:
+                shm.unlink()
 
 
 if __name__ == "__main__":

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 4
+#define SRT_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------------------------ */
 #define SRT_OK 0
@@ -237,6 +237,12 @@ typedef struct srt_render_args {
 #define SRT_RENDER_SHARDED 2
 /* with SRT_RENDER_SHARDED: gather the linear RGB as well (every rank passes the same flags) */
 #define SRT_RENDER_GATHER_RGB 4
+/* with SRT_RENDER_SHARDED, instead of SRT_RENDER_GATHER_RGB: every rank writes its own rows of the
+ * linear RGB straight into out_rgb, the whole frame's [3][height*width] buffer in host memory that
+ * all ranks share (e.g. POSIX shared memory registered in every process with srt_host_register),
+ * each over its own PCIe link; the RCCL gather to rank 0 then carries only the uint8 image.  The
+ * frame's linear RGB is complete in host memory when every rank's frame has finished. */
+#define SRT_RENDER_RGB_ROWS 8
 
 #define SRT_MAX_DEPTHS 64
 typedef struct srt_stats {
@@ -321,6 +327,10 @@ int srt_comm_barrier(srt_ctx* ctx);
 /* Pinned host memory (outputs of asynchronous frames are copied into it by the frame's stream). */
 int srt_host_alloc(srt_ctx* ctx, int64_t bytes, void** out);
 int srt_host_free(srt_ctx* ctx, void* ptr);
+/* Pin caller-owned host memory (e.g. a shared-memory frame for SRT_RENDER_RGB_ROWS) for the
+ * context's device, and release it again (hipHostRegister / hipHostUnregister). */
+int srt_host_register(srt_ctx* ctx, void* ptr, int64_t bytes);
+int srt_host_unregister(srt_ctx* ctx, void* ptr);
 /* Device memory helpers for callers that keep inputs resident in HBM (bench, multi-GPU). */
 int srt_device_alloc(srt_ctx* ctx, int64_t bytes, void** out);
 int srt_device_free(srt_ctx* ctx, void* ptr);

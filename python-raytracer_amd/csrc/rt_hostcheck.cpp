@@ -314,4 +314,16 @@ int hc_mt_uniforms(const uint32_t* key, int pos, int64_t n_out, int64_t n_skip, 
     return SRT_OK;
 }
 
+// x^J mod phi (rt_mt.h xpow_mod), 624 words
+void hc_xpow_mod(uint64_t J, uint32_t* out) {
+    const std::vector<uint32_t> p = rtmt::xpow_mod(J);
+    memcpy(out, p.data(), rtmt::N * 4);
+}
+
+// the window J words past `key` by the polynomial jump (rt_mt.h jump_serial with x^J)
+void hc_jump_window(const uint32_t* key, uint64_t J, uint32_t* out) {
+    const std::vector<uint32_t> p = rtmt::xpow_mod(J);
+    rtmt::jump_serial(key, p.data(), out);
+}
+
 }  // extern "C"

@@ -952,6 +952,7 @@ struct FrameSlot {
     hipEvent_t jit_ready = nullptr;  // recorded on the MT stream after this slot's jitter is generated
     hipEvent_t jit_free = nullptr;   // recorded on `stream` after the last kernel that reads the jitter
     bool jit_busy = false;           // `jit_free` guards the jitter buffer
+    uint32_t* mt_win = nullptr;      // segment windows of this slot's numpy-stream generation
     // ray queues: 2 x NSHARD segments of `seg` rays
     Queue q[2]{};
     int64_t seg = 0;
@@ -1028,7 +1029,10 @@ struct srt_ctx {
     int32_t* rows = nullptr;
     int64_t cam_cap[3] = {0, 0, 0};
     std::vector<uint8_t> cam_host[3];  // host copies of what xs / ys / rows hold
-    uint32_t* mt = nullptr;    // MT19937 jump tables (255 x 624), two round keys, two final windows, segment windows
+    uint32_t* mt = nullptr;    // MT19937 jump tables (255 x 624), two round keys, two final windows
+    // frame-end jump polynomial of the last pipelined frame shape (rt_mt.h xpow_mod / end_jump)
+    int64_t mt_end_words = -1;
+    uint32_t* mt_end_poly = nullptr;
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
@@ -1048,10 +1052,10 @@ struct srt_ctx {
     // pipelined frames: slots they rotate over (option "slots"); the numpy-stream generation of
     // single-pass frames on a stream of its own ("mt_stream"); host-output copies on a stream of
     // their own ("copy_stream").  ex1 1080p, host outputs, one MI355X, ms/frame: 3 slots 1.83; 2 slots
-    // + copy stream 1.83; 3 slots + MT stream 1.82; 2 slots 2.20; 2 slots + MT stream 2.00.  The
-    // default keeps three streams (HIP's default of four hardware queues per process, so no stream
-    // shares a queue)
-    int nslots = 3;
+    // + copy stream 1.83; 3 slots + MT stream 1.82; 2 slots 2.20; 2 slots + MT stream 2.00; one rank's
+    // shard of an 8-GPU frame (bench --shard-of 8, same box): 3 slots 0.627, 4 slots 0.544, 3 slots +
+    // MT stream 0.857.  Four slots (a stream each, HIP's default of four hardware queues per process)
+    int nslots = 4;
     bool use_mt_stream = false;
     bool use_copy_stream = false;
     FrameSlot* f = &slots[0];
@@ -1272,7 +1276,7 @@ int mt_ensure(srt_ctx* c) {
     if (c->mt) return SRT_OK;
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_jump),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)MT_LDS_BYTES));
-    HIP_TRY(dalloc(&c->mt, MT_NTAB + 4 * rtmt::N + (int64_t)rtmt::SEGS * rtmt::N));
+    HIP_TRY(dalloc(&c->mt, MT_NTAB + 4 * rtmt::N));
     HIP_TRY(hipMemcpy(c->mt, rtmt::tables_flat(), MT_NTAB * 4, hipMemcpyHostToDevice));
     return SRT_OK;
 }
@@ -1281,10 +1285,16 @@ int mt_ensure(srt_ctx* c) {
 // (device) and n_skip more draws; the window holding the last consumed word becomes mt_dump(c).  Returns the
 // numpy position of that window in *final_pos.  `plane` > 0: only the doubles of the planes
 // (index % 4) in `plane_mask` are stored (a pinhole camera reads no lens-disk pair).
-int mt_launch(srt_ctx* c, hipStream_t st, const uint32_t* key, int pos, int64_t n_out, int64_t n_skip, double* out, int* final_pos,
-              int64_t plane = 0, int plane_mask = 15) {
+// `win`: the segment-window table of this generation (SEGS x 624 words; per frame slot, as pipelined
+// frames generate concurrently).  `end_poly` (x^end_at mod phi, device) on a one-round generation:
+// k_mt_jump also makes the final window, and `key_ready` is recorded right after it -- the next
+// frame's generation may start then, beside this one's generators.
+int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, int pos, int64_t n_out, int64_t n_skip,
+              double* out, int* final_pos, int64_t plane = 0, int plane_mask = 15, const uint32_t* end_poly = nullptr,
+              int64_t end_at = 0, hipEvent_t key_ready = nullptr) {
     uint32_t* keys[2] = {c->mt + MT_NTAB, c->mt + MT_NTAB + rtmt::N};
     const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
+    if (plan.rounds.size() != 1) end_poly = nullptr;
     for (size_t r = 0; r < plan.rounds.size(); ++r) {
         const rtmt::Round& R = plan.rounds[r];
         MtArgs A{};
@@ -1301,13 +1311,22 @@ int mt_launch(srt_ctx* c, hipStream_t st, const uint32_t* key, int pos, int64_t 
         // the block's doubles span at most two planes when a plane holds >= 312 of them
         A.plane = plane >= 1024 ? plane : 0;
         A.plane_mask = plane_mask;
-        // segment windows (table after the keys and final windows), then the generators
-        uint32_t* win = c->mt + MT_NTAB + 4 * rtmt::N;
-        if (R.nseg > 1) {
-            hipLaunchKernelGGL(k_mt_jump, dim3(R.nseg - 1), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
+        // segment windows (and the final window), then the generators
+        const bool end = end_poly && A.dump_dst;
+        if (end) {
+            A.end_poly = end_poly;
+            A.end_at = end_at;
+        }
+        const int jump_blocks = (R.nseg - 1) + (end ? 1 : 0);
+        A.key_in_win = jump_blocks > 0;
+        if (jump_blocks > 0) {
+            hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
             HIP_TRY(hipGetLastError());
         }
-        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, A, (const uint32_t*)win);
+        if (end && key_ready) HIP_TRY(hipEventRecord(key_ready, st));
+        MtArgs G = A;
+        if (end) G.dump_dst = nullptr;  // (made by the jump kernel)
+        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, G, (const uint32_t*)win);
         HIP_TRY(hipGetLastError());
     }
     c->mt_cur ^= 1;
@@ -1397,7 +1416,8 @@ void free_slot(FrameSlot& f) {
     (void)hipStreamSynchronize(f.stream);
     free_list(f.queue_bufs);
     free_list(f.ring_bufs);
-    void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb};
+    void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb,
+                    f.mt_win};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -1473,7 +1493,7 @@ int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) {
 // every other rank's uint8 (and linear-RGB) tile, the others send theirs.
 int gather_post(srt_ctx* c) {
     const FrameSlot::Gather& G = c->f->gather;
-    if (!G.on || c->nranks == 1) return SRT_OK;
+    if (!G.on || c->nranks == 1 || !c->comm) return SRT_OK;  // (no communicator: a rehearsed shard)
     hipStream_t st = c->f->stream;
     if (c->rank == 0) {
         for (int q = 1; q < c->nranks; ++q) {
@@ -1505,7 +1525,7 @@ int gather_frame(srt_ctx* c) {
 // Rank 0, after the gather: the tiles into the frame, then to the caller's host buffers if any.
 int gather_finish(srt_ctx* c) {
     const FrameSlot::Gather& G = c->f->gather;
-    if (!G.on || c->rank != 0) return SRT_OK;
+    if (!G.on || c->rank != 0 || (c->nranks > 1 && !c->comm)) return SRT_OK;
     GatherTiles T{};
     for (int q = 0; q < c->nranks; ++q) {
         T.u8[q] = q == 0 ? c->f->u8 : c->f->g_u8 + (int64_t)q * G.maxpix * 3;
@@ -1570,7 +1590,7 @@ int srt_destroy(srt_ctx* c) {
     if (c->mt_done) (void)hipEventDestroy(c->mt_done);
     if (c->mt_stream) (void)hipStreamDestroy(c->mt_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red};
+    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_end_poly};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     delete c;
@@ -1586,6 +1606,20 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
+    if (!strcmp(key, "rehearse_shard")) {
+        // diagnostic: act as rank (value & 255) of (value >> 8) ranks without a communicator, so one
+        // GPU can render the shards of an N-rank frame in turn (no gather; SRT_RENDER_RGB_ROWS still
+        // writes the rank's rows into the host frame).  0 ends the rehearsal.
+        if (c->comm) return fail(SRT_ERR_ARG, "the context has a communicator");
+        const int n = value ? (int)(value >> 8) : 1, r = value ? (int)(value & 255) : 0;
+        if (n < 1 || n > MAX_RANKS || r >= n) return fail(SRT_ERR_ARG, "rehearse_shard: (nranks << 8) | rank");
+        HIP_TRY(hipSetDevice(c->device));
+        int rc = finish_async(c, nullptr);
+        if (rc) return rc;
+        c->nranks = n;
+        c->rank = r;
+        return SRT_OK;
+    }
     if (!strcmp(key, "slots") || !strcmp(key, "mt_stream") || !strcmp(key, "copy_stream")) {
         if (!strcmp(key, "slots") && (value < 1 || value > MAX_FRAME_SLOTS)) return fail(SRT_ERR_ARG, "slots: 1..4");
         HIP_TRY(hipSetDevice(c->device));
@@ -1732,8 +1766,11 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
-    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB))
+    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS))
         return fail(SRT_ERR_ARG, "unknown render flag");
+    if ((a->flags & SRT_RENDER_RGB_ROWS) &&
+        (!(a->flags & SRT_RENDER_SHARDED) || (a->flags & SRT_RENDER_GATHER_RGB) || !a->out_rgb))
+        return fail(SRT_ERR_ARG, "SRT_RENDER_RGB_ROWS needs SRT_RENDER_SHARDED, out_rgb and no SRT_RENDER_GATHER_RGB");
     const bool async = (a->flags & SRT_RENDER_ASYNC) != 0;
     const bool sharded = (a->flags & SRT_RENDER_SHARDED) != 0;
     if (a->spp <= 0 || cam->width <= 0 || cam->height <= 0 || (!sharded && a->n_rows <= 0) || !cam->xs || !cam->ys)
@@ -1777,6 +1814,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // outputs written by this rank: a shard's tiles stay on the device (the gather reads them); rank 0
     // of a sharded frame writes the whole frame to the caller's buffers after the gather
     const bool gather_rgb = sharded && (a->flags & SRT_RENDER_GATHER_RGB) != 0;
+    const bool rgb_rows = sharded && (a->flags & SRT_RENDER_RGB_ROWS) != 0;
+    if (rgb_rows && ptr_kind(a->out_rgb) != 2)
+        return fail(SRT_ERR_ARG, "SRT_RENDER_RGB_ROWS: out_rgb must be pinned or registered host memory");
     int rc;
     // samples per pass: both queues must hold spp_pass * npix * fanout rays
     const int64_t per_sample = npix * c->fanout;
@@ -1912,7 +1952,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // for the ex1 1080p RGB, against 28 GB/s for a resolve kernel storing straight into pinned
     // memory over PCIe); a shard resolves into its slot tiles (gathered afterwards)
     const bool rgb_direct = rk == 1, u8_direct = uk == 1;
-    double* res_rgb = sharded ? (gather_rgb ? c->f->rgb : nullptr) : a->out_rgb ? (rgb_direct ? a->out_rgb : c->f->rgb) : nullptr;
+    double* res_rgb = sharded ? ((gather_rgb || rgb_rows) ? c->f->rgb : nullptr)
+                              : a->out_rgb ? (rgb_direct ? a->out_rgb : c->f->rgb) : nullptr;
     uint8_t* res_u8 = sharded ? c->f->u8 : a->out_srgb8 ? (u8_direct ? a->out_srgb8 : c->f->u8) : nullptr;
     // only the depths this frame can reach are handed back and cleared per pass
     const int64_t used_words = std::min<int64_t>(F.cnt_words, (int64_t)(F.dcap + 2) * NSHARD);
@@ -1982,12 +2023,26 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 const int64_t n_out = (int64_t)ns * 4 * W * Hf;
                 const int64_t n_skip = (p + 1 == F.npass) ? 4 * W * Hf : 0;
                 if (p > 0) mt_key = mt_dump(c);  // the previous pass's final window
+                if (!c->f->mt_win && dalloc(&c->f->mt_win, (int64_t)rtmt::SEGS * rtmt::N) != hipSuccess)
+                    return fail(SRT_ERR_MEMORY, "window table allocation failed");
+                // a pipelined one-pass frame: its final window (the next frame's key) by one jump, so
+                // the next frame's generation starts once this one's jump kernel has run
+                const int64_t n_words = 2 * (n_out + n_skip);
+                const bool end = async && F.npass == 1 && n_words <= (int64_t)rtmt::SEGS * rtmt::L &&
+                                 rtmt::end_jump(n_words) > 0;
+                if (end && c->mt_end_words != n_words) {
+                    if (!c->mt_end_poly) HIP_TRY(dalloc(&c->mt_end_poly, rtmt::N));
+                    const std::vector<uint32_t> poly = rtmt::xpow_mod(rtmt::end_jump(n_words));
+                    HIP_TRY(hipMemcpy(c->mt_end_poly, poly.data(), rtmt::N * 4, hipMemcpyHostToDevice));
+                    c->mt_end_words = n_words;
+                }
                 // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
-                if ((rc = mt_launch(c, mst, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos, W * Hf,
-                                    cam->lens_radius != 0.0 ? 15 : 3)))
+                if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos, W * Hf,
+                                    cam->lens_radius != 0.0 ? 15 : 3, end ? c->mt_end_poly : nullptr,
+                                    end ? (int64_t)rtmt::end_jump(n_words) : 0, end ? c->mt_done : nullptr)))
                     return rc;
-                // the next frame's stream may start as soon as this one's is generated
-                if (p + 1 == F.npass) HIP_TRY(hipEventRecord(c->mt_done, mst));
+                // otherwise the next frame's stream may start as soon as this one's is generated
+                if (p + 1 == F.npass && !end) HIP_TRY(hipEventRecord(c->mt_done, mst));
                 if (mst != c->f->stream) {
                     HIP_TRY(hipEventRecord(c->f->jit_ready, mst));
                     HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->jit_ready, 0));
@@ -2085,6 +2140,24 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
         c->f->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
+        // this rank's rows of the linear RGB into the shared host frame: per plane, the full 8-row
+        // bands as one pitched copy (the rank's band b is frame rows 8 (b nranks + rank) ..), then a
+        // short last band
+        if (rgb_rows) {
+            const int64_t band_px = (int64_t)BAND * W;
+            const int64_t nb = npix / band_px, tail = npix - nb * band_px;
+            for (int pl = 0; pl < 3; ++pl) {
+                double* dst = a->out_rgb + (int64_t)pl * W * Hf;
+                const double* src = c->f->rgb + (int64_t)pl * npix;
+                if (nb > 0)
+                    HIP_TRY(hipMemcpy2DAsync(dst + (int64_t)c->rank * band_px, (size_t)(c->nranks * band_px * 8), src,
+                                             (size_t)(band_px * 8), (size_t)(band_px * 8), (size_t)nb,
+                                             hipMemcpyDeviceToHost, c->f->stream));
+                if (tail > 0)
+                    HIP_TRY(hipMemcpyAsync(dst + (nb * c->nranks + c->rank) * band_px, src + nb * band_px,
+                                           (size_t)(tail * 8), hipMemcpyDeviceToHost, c->f->stream));
+            }
+        }
         // the shard's tiles to rank 0 (RCCL over xGMI), assembled into the frame there
         FrameSlot::Gather& G = c->f->gather;
         G = FrameSlot::Gather{};
@@ -2394,7 +2467,9 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     hipStream_t st = c->f->stream;
     HIP_TRY(hipMemcpyAsync(mt_key0(c), key, rtmt::N * 4, hipMemcpyHostToDevice, st));
     int final_pos = 0;
-    if ((rc = mt_launch(c, st, mt_key0(c), pos, n_out, n_skip, dst, &final_pos))) return rc;
+    if (!c->f->mt_win && dalloc(&c->f->mt_win, (int64_t)rtmt::SEGS * rtmt::N) != hipSuccess)
+        return fail(SRT_ERR_MEMORY, "window table allocation failed");
+    if ((rc = mt_launch(c, st, c->f->mt_win, mt_key0(c), pos, n_out, n_skip, dst, &final_pos))) return rc;
     if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(key_out, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2536,6 +2611,22 @@ int srt_host_alloc(srt_ctx* c, int64_t bytes, void** out) {
     if (!c || !out || bytes <= 0) return fail(SRT_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    return SRT_OK;
+}
+
+int srt_host_register(srt_ctx* c, void* p, int64_t bytes) {
+    if (!c || !p || bytes <= 0) return fail(SRT_ERR_ARG, "null ctx/pointer or bad size");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipHostRegister(p, (size_t)bytes, hipHostRegisterPortable));
+    return SRT_OK;
+}
+
+int srt_host_unregister(srt_ctx* c, void* p) {
+    if (!c || !p) return fail(SRT_ERR_ARG, "null ctx/pointer");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = finish_async(c, nullptr);  // frames in flight may still write into it
+    if (rc) return rc;
+    HIP_TRY(hipHostUnregister(p));
     return SRT_OK;
 }
 

@@ -133,6 +133,95 @@ RT_MT_HD bool dumps(int s, int64_t d) {
     return lo && (d <= window_start(s + 1) || s == SEGS - 1);
 }
 
+// ---- jump polynomials for arbitrary distances (host) ----------------------------------------
+// x^J mod phi by left-to-right square-and-shift over GF(2): squaring spreads the bits, and phi is
+// sparse (~135 terms), so a reduction XORs each high 64-bit chunk back at the few term offsets.
+// A frame of a fixed shape consumes a fixed number of words, so the window at the end of frame k
+// (the next frame's key) is one jump from frame k's key: the pipelined generator of frame k+1 need
+// not wait for frame k's whole generation (rt_kernels.hip, k_mt_jump end block).
+constexpr int PW = 312;  // 64-bit words of a reduced polynomial (19968 bits >= 19937)
+struct Gf2 {
+    uint64_t w[2 * PW];  // products before reduction
+};
+
+inline const std::vector<int>& phi_terms() {  // exponents e < 19937 of phi's terms
+    static std::vector<int> t;
+    if (t.empty())
+        for (int i = 0; i < POLY_BITS; ++i)
+            if ((RT_MT_PHI[i >> 5] >> (i & 31)) & 1u) t.push_back(i);
+    return t;
+}
+
+inline void gf2_xor_at(uint64_t* a, uint64_t c, int64_t off) {  // a ^= c << off (bits)
+    const int64_t wi = off >> 6;
+    const int sh = (int)(off & 63);
+    a[wi] ^= c << sh;
+    if (sh) a[wi + 1] ^= c >> (64 - sh);
+}
+
+// reduce a (degree < 2 * 19968) modulo phi, in place; the result occupies words [0, PW)
+inline void gf2_reduce(Gf2& a) {
+    const std::vector<int>& terms = phi_terms();
+    for (int i = 2 * PW - 1; i >= POLY_BITS / 64; --i) {
+        for (;;) {
+            int64_t base = (int64_t)64 * i - POLY_BITS;  // bit j of word i sits at x^(19937 + base + j)
+            uint64_t c = a.w[i];
+            if (base < 0) c &= ~0ull << (-base);  // (the boundary word: only bits >= 19937)
+            if (!c) break;
+            a.w[i] ^= c;
+            if (base < 0) {
+                c >>= -base;
+                base = 0;
+            }
+            for (int e : terms) gf2_xor_at(a.w, c, base + e);  // x^19937 = sum of the other terms
+        }
+    }
+}
+
+inline uint64_t gf2_spread32(uint32_t v) {  // bit j -> bit 2j
+    uint64_t x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+// x^J mod phi as 624 32-bit words (bit i = word i/32, bit i%32), the layout of RT_MT_JD
+inline std::vector<uint32_t> xpow_mod(uint64_t J) {
+    Gf2 r{};
+    r.w[0] = 1;
+    for (int b = 63; b >= 0; --b) {
+        if (!(J >> b) && b > 0) continue;  // (skip leading zeros; x^0 = 1)
+        Gf2 q{};
+        for (int k = 0; k < PW; ++k) {
+            q.w[2 * k] = gf2_spread32((uint32_t)r.w[k]);
+            q.w[2 * k + 1] = gf2_spread32((uint32_t)(r.w[k] >> 32));
+        }
+        gf2_reduce(q);
+        if ((J >> b) & 1) {
+            for (int k = PW; k > 0; --k) q.w[k] = (q.w[k] << 1) | (q.w[k - 1] >> 63);
+            q.w[0] <<= 1;
+            gf2_reduce(q);
+        }
+        r = q;
+    }
+    std::vector<uint32_t> out(N);
+    for (int k = 0; k < N; ++k) out[k] = (uint32_t)(r.w[k >> 1] >> (32 * (k & 1)));
+    return out;
+}
+
+// Where the next frame's key window lies for a frame of n_words words: the final window of a
+// generation from position pos is at word 624 floor((pos + n_words - 1) / 624) of its key window,
+// one of two values over pos in [1, 624].  end_jump is a window position 1249 .. 1873 words before
+// it for every pos (J = 624 m - 1 from the table's convention), so the end block jumps to J with
+// x^J and generates at most four blocks to reach the final window; 0 when the frame is too short.
+inline uint64_t end_jump(int64_t n_words) {
+    const int64_t base = (int64_t)N * ((n_words - 1) / N);
+    return base >= 2 * (int64_t)N + 1 ? (uint64_t)(base - 2 * N - 1) : 0;
+}
+
 // ---- serial reference (host test driver) ------------------------------------------------------
 // raw words generated forward from window `w` (624 words, w[0] = word at absolute index `start`)
 struct SerialStream {

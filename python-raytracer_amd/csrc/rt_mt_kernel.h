@@ -24,6 +24,10 @@ struct MtArgs {
     int64_t plane;         // doubles per jitter plane (0: write every double)
     int32_t plane_mask;    // bit k set: write the doubles of planes with index % 4 == k
     int32_t pos;           // outputs start at word `pos` of the key window
+    const uint32_t* end_poly;  // x^end_at mod phi: k_mt_jump's last block makes the final window (dump_dst)
+    int64_t end_at;            // window position of that jump
+    int32_t key_in_win;        // the key window is copied to win[0] by k_mt_jump (segment 0 reads it there)
+    int32_t pad_;
 };
 
 // Two launches per round.
@@ -45,7 +49,7 @@ constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623
 constexpr int MT_RED = 640;                           // per-wave stride of the reduction buffer
 static_assert(MT_CW_PER_WAVE * MT_WAVES == rtmt::N, "coefficient words split evenly over the waves");
 static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 42 <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
-static_assert(MT_WAVES * MT_RED <= MT_YBLOCKS * rtmt::N, "the reduction aliases y");
+static_assert(MT_WAVES * MT_RED + 3 * rtmt::N <= MT_YBLOCKS * rtmt::N, "the reduction and end ring alias y");
 constexpr size_t MT_LDS_BYTES = (size_t)(MT_YBLOCKS + 1) * rtmt::N * 4;  // y + coefficient words
 // generator threads per segment: 5 waves (227 make the next block, 312 store the current one).
 // Measured (222 segments, ex1 1080p pinhole planes): 1 wave 1.17 ms, 4 waves 0.64, 5 waves 0.50,
@@ -113,16 +117,23 @@ __device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
     return g;
 }
 
-// block s - 1 of the grid: the window of segment s >= 1 into win + 624 s
+// block s - 1 of the grid: the window of segment s >= 1 into win + 624 s.  With A.end_poly the last
+// block instead jumps to the window at A.end_at and generates forward to the final window (A.dump_at),
+// written to A.dump_dst: the next frame's key, ready when this kernel ends (its whole generation need
+// not have run).  Block 0 also copies the key window to win[0] for segment 0's generator.
 __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win) {
     extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words (+ 624 coefficient words)
     uint32_t* y = mt_lds;
     uint32_t* coef = mt_lds + MT_YBLOCKS * rtmt::N;
-    uint32_t* red = mt_lds;  // MT_WAVES x MT_RED (aliases y once it is read)
+    uint32_t* red = mt_lds;                   // MT_WAVES x MT_RED (aliases y once it is read)
+    uint32_t* ring = mt_lds + MT_WAVES * MT_RED;  // end block: 3 blocks after the reduction
+    const bool end_block = A.end_poly && blockIdx.x == gridDim.x - 1;
     const int s = blockIdx.x + 1;
     const int t = threadIdx.x;
-    if (mt_seg(A, s).idle()) return;
-    const uint32_t* poly = A.tab + (int64_t)(s - 1) * rtmt::N;
+    if (blockIdx.x == 0)
+        for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
+    if (!end_block && mt_seg(A, s).idle()) return;
+    const uint32_t* poly = end_block ? A.end_poly : A.tab + (int64_t)(s - 1) * rtmt::N;
     for (int m = t; m < rtmt::N; m += MT_THREADS) {
         y[m] = A.key[m];
         coef[m] = poly[m];
@@ -164,7 +175,25 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
         uint32_t w = 0u;
 #pragma unroll
         for (int v = 0; v < MT_WAVES; ++v) w ^= red[v * MT_RED + m];
-        win[(int64_t)s * rtmt::N + m] = w;
+        if (end_block)
+            ring[m] = w;
+        else
+            win[(int64_t)s * rtmt::N + m] = w;
+    }
+    if (!end_block) return;
+    // end block: generate from the window at end_at until the final window is written
+    __syncthreads();
+    int slot = 0;
+    for (int64_t b0 = A.end_at; b0 < A.dump_at + rtmt::N; b0 += rtmt::N) {
+        const uint32_t* cur = ring + slot * rtmt::N;
+        const int next = slot == 2 ? 0 : slot + 1;
+        if (b0 + rtmt::N < A.dump_at + rtmt::N) mt_next_block(cur, ring + next * rtmt::N, t);
+        for (int m = t; m < rtmt::N; m += MT_THREADS) {
+            const int64_t x = b0 + m;
+            if (x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = cur[m];
+        }
+        slot = next;
+        mt_barrier();
     }
 }
 
@@ -178,7 +207,7 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
     const int lane = threadIdx.x;
     const MtSeg g = mt_seg(A, s);
     if (g.idle()) return;
-    const uint32_t* w0p = s == 0 ? A.key : win + (int64_t)s * rtmt::N;
+    const uint32_t* w0p = (s == 0 && !A.key_in_win) ? A.key : win + (int64_t)s * rtmt::N;
     for (int m = lane; m < rtmt::N; m += NT) ring[m] = w0p[m];
     __syncthreads();
     // block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it holds

@@ -209,8 +209,8 @@ class TraceArgs(ctypes.Structure):
 
 
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
-RENDER_ASYNC, RENDER_SHARDED, RENDER_GATHER_RGB = 1, 2, 4  # SRT_RENDER_*
-ABI_VERSION = 4  # SRT_ABI_VERSION of include/sightpy_rt.h
+RENDER_ASYNC, RENDER_SHARDED, RENDER_GATHER_RGB, RENDER_RGB_ROWS = 1, 2, 4, 8  # SRT_RENDER_*
+ABI_VERSION = 5  # SRT_ABI_VERSION of include/sightpy_rt.h
 COMM_ID_BYTES = 128
 
 SIGNATURES = {
@@ -243,6 +243,8 @@ SIGNATURES = {
     "srt_comm_barrier": (ctypes.c_int, [_p]),
     "srt_host_alloc": (ctypes.c_int, [_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),
     "srt_host_free": (ctypes.c_int, [_p, _p]),
+    "srt_host_register": (ctypes.c_int, [_p, _p, ctypes.c_int64]),
+    "srt_host_unregister": (ctypes.c_int, [_p, _p]),
     "srt_last_error": (ctypes.c_char_p, []),
 }
 

@@ -31,6 +31,8 @@ def lib():
         _lib.hc_primary_rays.argtypes = [ctypes.POINTER(N.CameraDesc)] + [ctypes.c_void_p] * 3
         _lib.hc_mt_uniforms.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        _lib.hc_xpow_mod.argtypes = [ctypes.c_uint64, ctypes.c_void_p]
+        _lib.hc_jump_window.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         _lib.hc_last_error.restype = ctypes.c_char_p
         _lib.hc_philox.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
         _lib.hc_mix32.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
@@ -109,6 +111,21 @@ def mt_uniforms(key, pos, n_out, n_skip=0):
                               key_out.ctypes.data, ctypes.byref(pos_out))
     assert rc == 0, rc
     return out, key_out, pos_out.value
+
+
+def xpow_mod(J):
+    """rt_mt.h xpow_mod: x^J mod phi as 624 uint32 words."""
+    out = np.empty(624, dtype=np.uint32)
+    lib().hc_xpow_mod(int(J), out.ctypes.data)
+    return out
+
+
+def jump_window(key, J):
+    """The MT19937 window J words past `key` by rt_mt.h's polynomial jump (exact from word 1 on)."""
+    key = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.empty(624, dtype=np.uint32)
+    lib().hc_jump_window(key.ctypes.data, int(J), out.ctypes.data)
+    return out
 
 
 def philox(ctr, k0, k1):

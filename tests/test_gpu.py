@@ -277,6 +277,44 @@ def test_gpu_async_frames_match_sync_frame():
     assert np.array_equal(u8.reshape(120, 160, 3), ref.srgb8)
 
 
+def test_gpu_async_numpy_stream_frames_match_sync_frames():
+    """Pipelined frames drawing numpy's stream on the device (the bench's frame loop): each frame's key
+    window comes from the previous frame's end jump (k_mt_jump's last block) while that frame's
+    generators still run.  Every frame equals the synchronous render from the same numpy state, and
+    numpy's state after the sequence equals the state after the synchronous frames."""
+    import ctypes
+    from sightpy import _native as N
+
+    B = _backend()
+    sc = scenes.example1(160, 120, 4)
+    K, spp, npix = 5, 2, 160 * 120
+    np.random.seed(7)
+    ref = [B.render_scene(sc, spp, seed=5, mt=True) for _ in range(K)]
+    want_state = np.random.get_state()
+    np.random.seed(7)
+    mt = N.MtState.from_numpy()
+    lib, ctx = B.context()
+    B.upload(sc)
+    cd = B.camera_desc(sc.camera)
+    bufs = [(B.device_buffer("mt_rgb%d" % k, 3 * npix * 8), B.device_buffer("mt_u8%d" % k, 3 * npix)) for k in range(K)]
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, 120, 0
+    a.jitter, a.seed, a.out_hit_id, a.rows = None, 5, None, None
+    a.mt = ctypes.pointer(mt)
+    a.flags = N.RENDER_ASYNC
+    for k in range(K):
+        a.out_rgb, a.out_srgb8 = bufs[k]
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+    N.check(lib, lib.srt_render_finish(ctx, None))
+    mt.to_numpy()
+    got_state = np.random.get_state()
+    assert got_state[2] == want_state[2] and np.array_equal(got_state[1], want_state[1])
+    for k in range(K):
+        rgb = np.empty((3, npix))
+        N.check(lib, lib.srt_memcpy(ctx, N.ptr(rgb), bufs[k][0], rgb.nbytes))
+        np.testing.assert_allclose(rgb, ref[k].rgb, rtol=1e-12, atol=1e-15)
+
+
 @pytest.mark.parametrize("mode", ["wavefront", "frame"])
 def test_gpu_triangle_mesh_bvh_matches_oracle(tmp_path, mode):
     """TriangleMesh through the device BVH (320 triangles + a tie-making duplicate set) against the

@@ -114,3 +114,27 @@ def test_scene_render_device_stream_equals_host_stream():
     d = np.abs(a.astype(int) - b.astype(int))
     assert d.max() <= 1 and (d > 0).mean() < 1e-3
     assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
+
+
+def test_host_jump_polynomials():
+    """rt_mt.h xpow_mod (square-and-shift modulo the sparse phi) reproduces the tabulated jumps
+    x^(sL - 1), and a jump by x^J lands on the window J words ahead of numpy's generator (the frame-end
+    jump that lets pipelined frames start their stream before the previous frame's is generated)."""
+    import re
+
+    src = (ROOT / "python-raytracer_amd" / "csrc" / "rt_mt_jump.h").read_text()
+    body = src.split("static const uint32_t RT_MT_JD")[1].split("};")[0]
+    rows = re.findall(r"\{(0x[^{}]*)\}", body)
+    for s in (1, 2, 200):
+        want = np.array([int(v, 16) for v in rows[s - 1].split(",")], dtype=np.uint32)
+        assert np.array_equal(HC.xpow_mod(s * (1 << 19) - 1), want)
+    rs = np.random.RandomState(11)
+    key = rs.get_state()[1]
+    for J in (623, 5000, 3 * 624 * 1000 + 17):
+        got = HC.jump_window(key, J)
+        # numpy's raw words J .. J + 623 after the key window (words 0..623): regenerate with pure Python
+        sys.path.insert(0, str(ROOT / "tools"))
+        import gen_mt_jump as G
+
+        words = G.raw_words([int(v) for v in key], J + 624)
+        assert np.array_equal(got[1:], np.array(words[J + 1:J + 624], dtype=np.uint32))

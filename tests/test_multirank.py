@@ -240,3 +240,47 @@ def test_gpu_every_shard_of_an_n_rank_frame_assembles_to_the_plain_render(world)
         assert np.array_equal(np.random.get_state()[1], after)
         rgb[:, rows] = part.rgb.reshape(3, len(rows), 120)
     np.testing.assert_allclose(rgb.reshape(3, -1), full.rgb, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world):
+    """SRT_RENDER_RGB_ROWS (the multi-GPU bench's output path): each rank writes its own rows of the
+    linear RGB into one host frame with pitched copies.  Rehearsed on one card (option
+    rehearse_shard: act as rank r of N without a communicator): the N shards, rendered in turn into
+    one pinned host frame, fill every row exactly once and equal the single-GPU frame."""
+    import ctypes
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    W, H, spp = 120, 70, 2  # 70 rows: a short last band
+    sc = scenes.example1(W, H, 4)
+    np.random.seed(4)
+    full = B.render_scene(sc, spp, seed=5, mt=True)
+    lib, ctx = B.context()
+    B.upload(sc)
+    cd = B.camera_desc(sc.camera)
+    host = ctypes.c_void_p()
+    N.check(lib, lib.srt_host_alloc(ctx, 3 * W * H * 8, ctypes.byref(host)))
+    try:
+        frame = np.ctypeslib.as_array((ctypes.c_double * (3 * W * H)).from_address(host.value))
+        frame[:] = np.nan
+        for r in range(world):
+            N.check(lib, lib.srt_set_option(ctx, b"rehearse_shard", (world << 8) | r))
+            np.random.seed(4)
+            st = N.MtState.from_numpy()
+            a = N.RenderArgs()
+            a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, H, 0
+            a.rows = a.jitter = a.out_srgb8 = a.out_hit_id = None
+            a.mt = ctypes.pointer(st)
+            a.seed = 5
+            a.out_rgb = host
+            a.flags = N.RENDER_SHARDED | N.RENDER_RGB_ROWS
+            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+        N.check(lib, lib.srt_set_option(ctx, b"rehearse_shard", 0))
+        assert not np.isnan(frame).any()
+        np.testing.assert_allclose(frame.reshape(3, -1), full.rgb, rtol=1e-12, atol=1e-15)
+    finally:
+        lib.srt_set_option(ctx, b"rehearse_shard", 0)
+        lib.srt_host_free(ctx, host)
