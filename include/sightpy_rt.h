@@ -15,6 +15,14 @@
  *   srt_intersect_collider <- Collider.intersect(O, D) sightpy/geometry/collider.py:12-14
  *                             (sphere.py:26-52, plane.py:57-90, cuboid.py:105-140,
  *                              triangle.py:36-66)
+ *   srt_shade              <- Material.get_color(scene, ray, hit) at given hits
+ *                             (material.py:43, glossy.py:25, refractive.py:24, diffuse.py:25,
+ *                              thin_film_interference.py:24, emissive.py:21; the children it
+ *                              spawns are traced as in get_raycolor)
+ *   srt_collider_surface   <- Collider.get_Normal(hit) / Collider.get_uv(hit) / Primitive.get_uv
+ *                             (sphere.py:17,54-64, plane.py:34,98-105, cuboid.py:29,142-187,
+ *                              triangle.py:85, skybox.py:29)
+ *   srt_texture_lookup     <- image.get_color(hit)     sightpy/textures/texture.py:32-39
  *   srt_primary_rays       <- Camera.get_ray(n)       sightpy/camera.py:51-85
  *   srt_upload_scene       <- (scene lowering; the reference deep-copies the Scene per task,
  *                              scene.py:85)
@@ -293,6 +301,24 @@ int srt_nearest(srt_ctx* ctx, const double* origin, const double* dir, int64_t n
                 int32_t* id, double* orient);
 int srt_intersect_collider(srt_ctx* ctx, const srt_collider* collider, const double* origin,
                            const double* dir, int64_t n, double* out /* [2][n] */);
+/* Material.get_color at the caller's hits: ray i is shaded as if its nearest hit were collider
+ * collider[i] at distance t[i] with orientation orient[i] (the values srt_nearest returns;
+ * -1 = no hit, nothing added), with no tie resolution; the reflected/refracted/diffuse rays
+ * it spawns are traced by get_raycolor's rules.  out_rgb[3][n] as srt_trace.  A collider index
+ * outside the scene fails with SRT_ERR_INDEX. */
+int srt_shade(srt_ctx* ctx, const srt_trace_args* args, const int32_t* collider, const double* t,
+              const double* orient, srt_stats* stats);
+/* Collider.get_Normal (N [3][n]) and get_uv (uv [2][n], u then v) at points P [3][n] on the
+ * collider; primitive_uv = 1 applies a Cuboid/SkyBox primitive's (4, 3) cross divide
+ * (SRT_CF_UV_CROSS, cuboid.py:29-34), 0 returns the collider's own coordinates.  Either output may
+ * be NULL.  Triangle uv is undefined in the reference (triangle.py:79-83): SRT_ERR_ARG. */
+int srt_collider_surface(srt_ctx* ctx, const srt_collider* collider, const double* P, int64_t n,
+                         double* N, double* uv, int primitive_uv);
+/* image.get_color: the texel at uv [2][n] of the texture record `tex` over `texels`
+ * (texel_bytes bytes, tex->offset into it), rgb [3][n] in [0, 1].  Indices outside the image
+ * fail with SRT_ERR_INDEX as numpy indexing raises. */
+int srt_texture_lookup(srt_ctx* ctx, const srt_texture* tex, const uint8_t* texels, int64_t texel_bytes,
+                       const double* uv, int64_t n, double* rgb);
 int srt_primary_rays(srt_ctx* ctx, const srt_camera* cam, const double* jitter /* [4][n] */,
                      double* origin /* [3][n] */, double* dir /* [3][n] */);
 /* numpy's legacy global-RNG stream on the device: writes the n_out doubles that

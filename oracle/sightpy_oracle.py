@@ -629,6 +629,31 @@ def trace_linear(scene, O, D, n, depth, dfl=0, stream=None):
         _RNG["stream"] = None
 
 
+def shade_linear(scene, ci, O, D, n, depth, t, orient, dfl=0, stream=None):
+    """Material.get_color at given hits (srt_shade): ray i shaded by collider ci[i] (-1: nothing)
+    at distance t[i], orientation orient[i], as material.get_color(scene, ray.extract(hit_check),
+    hit_info) in ray.py:131-146 with the hit supplied by the caller; children traced by raycolor."""
+    r = Rays(O, D, n, depth, dfl)
+    counts = {}
+    _RNG["stream"] = stream
+    try:
+        k = D.shape[1]
+        if stream is not None:
+            r.pix = np.arange(k, dtype=np.uint32)
+            r.path = mix32(TRACE_PATH, np.arange(k, dtype=np.uint32))
+        color = np.zeros((3, k))
+        for i, c in enumerate(scene.collider_list):
+            hit = ci == i
+            if np.any(hit):
+                sub = r.take(hit)
+                if stream is not None:
+                    sub.rnd = np.zeros(int(hit.sum()), dtype=np.int64)
+                color = color + place(shade(scene, c, sub, t[hit], orient[hit], counts), hit)
+        return color, counts
+    finally:
+        _RNG["stream"] = None
+
+
 def srgb_u8(rgb_lin, H, W):  # colour_functions.py:4-18 + scene.py:125-140
     rgb = np.where(rgb_lin <= 0.00304, 12.92 * rgb_lin, 1.055 * np.power(rgb_lin, 1.0 / 2.4) - 0.055)
     peak = np.amax(rgb, axis=0) + 0.00001

@@ -59,12 +59,13 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 800;
+constexpr size_t TRACE_PARAMS_BYTES = 832;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
 constexpr uint32_t RETRY_OVERFLOW = 1u;
 constexpr uint32_t RETRY_CHAIN_TIE = 2u;
+constexpr uint32_t RETRY_FIXED_RANGE = 4u;  // a contribution beyond the fixed-point range (fx_add)
 
 struct Queue {
     double *ox, *oy, *oz, *dx, *dy, *dz, *wr, *wg, *wb;
@@ -79,7 +80,9 @@ struct TraceParams {
     uint32_t* cnt_out;       // [NSHARD] append counters of the output shards (depth d+1)
     uint32_t* flags;         // [0] error bits, [1] overflow
     unsigned long long* shadow;
-    double* fb;              // [3][npix]
+    double* fb;              // [3][npix] depth-0 colour (stored by the pixel's own thread)
+    unsigned long long* fbx; // [3][npix] fixed-point sums of every added contribution (fb_add), or null:
+                             // f64 atomics into fb (option "deterministic" 0, order-dependent rounding)
     int64_t npix;
     int64_t seg;             // capacity of one queue shard (rays)
     uint64_t seed;
@@ -108,6 +111,10 @@ struct TraceParams {
     int dcap;             // deepest depth traced; deeper children are counted and dropped
     int fuse_resolve;     // 1: k_frame resolves its pixels (no framebuffer); 0: adds to fb
     int spp_total;        // samples of the frame (resolve average)
+    // k_shade_forced (srt_shade, Material.get_color): the first depth's hit per ray (index = pix)
+    const int32_t* force_id;
+    const double* force_t;
+    const double* force_o;
 };
 // kernel argument: host and device passes must agree on the layout (catches address-space pointer
 // size differences, see SceneView)
@@ -140,15 +147,45 @@ __device__ __forceinline__ Ray queue_load(const Queue& q, int64_t i) {
     return r;
 }
 
-__device__ __forceinline__ void fb_add(double* fb, int64_t npix, uint32_t pix, d3 w, d3 c) {
-    if (is_zero(c)) return;  // adding an exact zero is a no-op (framebuffer starts at +0.0)
+// Contributions added to a pixel by other threads (depth >= 1, split samples) go into an
+// order-independent fixed-point sum, so a frame is bit-reproducible (the reference is
+// deterministic; f64 atomics are not, their rounding depends on arrival order): each contribution
+// rounded to a multiple of 2^-FX_BITS and summed with one int64 atomic per channel (the count of f64
+// atomics it replaces); the resolve adds sum 2^-FX_BITS to the depth-0 colour.  Rounding error
+// <= 2^-45 = 2.8e-14 per contribution; a contribution of magnitude >= 2^17 (sums up to 2^19 stay in
+// range) raises RETRY_FIXED_RANGE and the frame is rendered again with f64 atomics.
+constexpr int FX_BITS = 44;
+constexpr double FX_SCALE = (double)(1ull << FX_BITS);
+constexpr double FX_UNIT = 1.0 / FX_SCALE;
+constexpr double FX_MAX = 131072.0;                 // 2^17
+
+__device__ __forceinline__ bool fx_add(unsigned long long* acc, double v) {
+    if (!(fabs(v) < FX_MAX)) return false;  // (also NaN)
+    atomicAdd(acc, (unsigned long long)__double2ll_rn(v * FX_SCALE));
+    return true;
+}
+
+__device__ __forceinline__ void fb_add(double* fb, unsigned long long* fbx, uint32_t* flags, int64_t npix,
+                                       uint32_t pix, d3 w, d3 c) {
+    if (is_zero(c)) return;  // adding an exact zero is a no-op
 #ifdef RT_ABL_FB  // diagnostic build only: no framebuffer atomics
     if (w.x * c.x == 12345.678) fb[pix] = 0.0;
     return;
 #endif
-    unsafeAtomicAdd(fb + pix, w.x * c.x);
-    unsafeAtomicAdd(fb + npix + pix, w.y * c.y);
-    unsafeAtomicAdd(fb + 2 * npix + pix, w.z * c.z);
+    if (fbx) {
+        // all three channels added (no short-circuit), then one range check
+        const int ok = (int)fx_add(fbx + pix, w.x * c.x) & (int)fx_add(fbx + npix + pix, w.y * c.y) &
+                       (int)fx_add(fbx + 2 * npix + pix, w.z * c.z);
+        if (!ok) atomicOr(flags + 1, RETRY_FIXED_RANGE);
+    } else {
+        unsafeAtomicAdd(fb + pix, w.x * c.x);
+        unsafeAtomicAdd(fb + npix + pix, w.y * c.y);
+        unsafeAtomicAdd(fb + 2 * npix + pix, w.z * c.z);
+    }
+}
+
+__device__ __forceinline__ double fx_value(const unsigned long long* fbx, int64_t npix, int ch, int64_t p) {
+    return (double)(long long)fbx[ch * npix + p] * FX_UNIT;
 }
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
@@ -193,7 +230,7 @@ struct GpuEmit {
         if (acc) {
             if (!is_zero(c)) *acc = add(*acc, mul(r.w, c));
         } else {
-            fb_add(P.fb, P.npix, r.pix, r.w, c);
+            fb_add(P.fb, P.fbx, P.flags, P.npix, r.pix, r.w, c);
         }
     }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
@@ -253,7 +290,7 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
 // MATS: material types compiled into this instantiation (the host picks one covering the scene).
 // Em: the emitter (GpuEmit: wavefront queues; FrameEmit: the frame kernel's per-wave ring); `em0`
 // is round 0's, tied colliders get copies with rounds 1, 2, ...
-template <uint32_t MATS, class Em>
+template <uint32_t MATS, class Em, bool FORCED = false>
 __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool active, uint32_t& err, int32_t* hit_slot,
                                           const Em& em0) {
     const SceneView& S = P.S;
@@ -261,7 +298,19 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     bool ties = false;
     int id = -1;
     RT_T0(tn0);
-    if (active) id = nearest_hit<(MATS & MAT_BVH) != 0>(S, r.o, r.d, t, o, ties);
+    if (FORCED) {  // the caller's hit (Material.get_color): that collider only, no tie loop
+        if (active) {
+            id = P.force_id[r.pix];
+            t = P.force_t[r.pix];
+            o = P.force_o[r.pix];
+            if (id < -1 || id >= (int32_t)S.ncol) {  // not a collider of the scene (IndexError)
+                err |= ERR_INDEX;
+                id = -1;
+            }
+        }
+    } else if (active) {
+        id = nearest_hit<(MATS & MAT_BVH) != 0>(S, r.o, r.d, t, o, ties);
+    }
     RT_ACC(1, tn0);
     if (hit_slot && active) *hit_slot = id;
     const Em& em = em0;
@@ -312,7 +361,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     }
     RT_ACC(2, tw0);
     // colliders tied at the same distance are all shaded and their colours added (ray.py:131-146)
-    if (__ballot(ties)) {
+    if (!FORCED && __ballot(ties)) {
         // wave-uniform collider loop (scalar table loads); lanes act on later colliders at t
         uint32_t round = 1;
         for (int c = 0; c < S.ncol; ++c) {
@@ -382,11 +431,15 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             RT_ACC(3, tt0);
         }
         if (ngroups > 1) {
-            if (active) fb_add(P.fb, P.npix, p, d3{1.0, 1.0, 1.0}, acc);
+            if (active) fb_add(P.fb, P.fbx, P.flags, P.npix, p, d3{1.0, 1.0, 1.0}, acc);
         } else if (active && P.fb_first) {
             P.fb[p] = acc.x;
             P.fb[P.npix + p] = acc.y;
             P.fb[2 * P.npix + p] = acc.z;
+            if (P.fbx) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = 0ull;  // this frame's fixed-point sums start here
+            }
         } else if (active && !is_zero(acc)) {
             P.fb[p] += acc.x;
             P.fb[P.npix + p] += acc.y;
@@ -411,7 +464,7 @@ struct ChainEmit {
     Ray* next;
     bool* has;
 
-    __device__ void local(d3 c) const { fb_add(P.fb, P.npix, r.pix, r.w, c); }
+    __device__ void local(d3 c) const { fb_add(P.fb, P.fbx, P.flags, P.npix, r.pix, r.w, c); }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void put(const Child& c, uint32_t path) const {
         if (*has) {
@@ -485,6 +538,35 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
             }
         }
         RT_ACC(14, tt1);
+    }
+    if (err) atomicOr(&P.flags[0], err);
+    if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+}
+
+// srt_shade's first depth: each queued ray shaded at the caller's hit (Material.get_color,
+// material.py:42-44), its children appended for the ordinary k_trace depths
+template <uint32_t MATS>
+__global__ __launch_bounds__(BLOCK) void k_shade_forced(TraceParams P0) {
+    TraceParams P = P0;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
+    const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
+    if (blk * BLOCK >= n) return;
+    stage_luts(P);
+    uint32_t err = 0;
+    uint32_t shadow = 0;
+    const int64_t off = (int64_t)shard * P.seg;
+    for (int64_t base = blk * BLOCK; base < n; base += nblk * BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const bool active = i < n;
+        Ray r;
+        if (active) {
+            r = queue_load(P.qin, off + i);
+        } else {
+            r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
+            r.pix = 0; r.meta = 0; r.path = 0;
+        }
+        trace_one<MATS, GpuEmit, true>(P, r, active, err, nullptr, GpuEmit{P, r, shard, 0u, &shadow, nullptr});
     }
     if (err) atomicOr(&P.flags[0], err);
     if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
@@ -776,7 +858,8 @@ __global__ __launch_bounds__(BLOCK) void k_pass_end(uint32_t* counts, int64_t wo
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npix, unsigned long long* shadow,
+__global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, const unsigned long long* fbx, int64_t npix,
+                                                  unsigned long long* shadow,
                                                   uint32_t* shadow_host, double spp, double* rgb, uint8_t* u8,
                                                   uint32_t* counts, int64_t words, uint32_t* flags, uint32_t* host,
                                                   uint32_t* host_flags) {
@@ -813,13 +896,27 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, int64_t npi
         const int n = (int)min<int64_t>(64, npix - p0);
         uint8_t px[3] = {0, 0, 0};
         if (p < npix) {
-            double r = fb[p] / spp, g = fb[npix + p] / spp, b = fb[2 * npix + p] / spp;
+            double r = fb[p], g = fb[npix + p], b = fb[2 * npix + p];
+            if (fbx) {  // the contributions added by other threads (fixed point, order-independent)
+                r += fx_value(fbx, npix, 0, p);
+                g += fx_value(fbx, npix, 1, p);
+                b += fx_value(fbx, npix, 2, p);
+            }
+            r /= spp;
+            g /= spp;
+            b /= spp;
             double a0, a1, a2;
             resolve_pixel(r, g, b, a0, a1, a2, px);
             if (rgb) { rgb[p] = r; rgb[npix + p] = g; rgb[2 * npix + p] = b; }
         }
         if (u8) store_u8_chunk(u8 + 3 * p0, px, lane, n);
     }
+}
+
+// fb += the fixed-point sums (srt_trace's colours)
+__global__ __launch_bounds__(BLOCK) void k_fx_combine(double* fb, const unsigned long long* fbx, int64_t npix) {
+    for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK)
+        for (int ch = 0; ch < 3; ++ch) fb[ch * npix + p] += fx_value(fbx, npix, ch, p);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O, const double* D, int64_t n, double* t,
@@ -847,6 +944,41 @@ __global__ __launch_bounds__(BLOCK) void k_intersect_one(const srt_collider* c_g
         out[i] = t;
         out[n + i] = orient;
     }
+}
+
+// Collider.get_Normal / get_uv and Primitive.get_uv at points P (the reference's per-hit plugin
+// points, collider.py:12-17, sphere.py:54-64, plane.py:98-105, cuboid.py:142-187, skybox.py:29-32)
+__global__ __launch_bounds__(BLOCK) void k_collider_surface(const srt_collider* c_generic, const double* P, int64_t n,
+                                                           double* N, double* uv) {
+    const RT_RO srt_collider* c = (const RT_RO srt_collider*)c_generic;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        const d3 p = d3{P[i], P[n + i], P[2 * n + i]};
+        if (N) {
+            const d3 v = collider_normal(*c, p);
+            N[i] = v.x;
+            N[n + i] = v.y;
+            N[2 * n + i] = v.z;
+        }
+        if (uv) {
+            double u = 0.0, v = 0.0;
+            collider_uv(*c, p, u, v);
+            uv[i] = u;
+            uv[n + i] = v;
+        }
+    }
+}
+
+// image.get_color(hit): the texel of (u, v) through texture 0 of S (texture.py:27-39)
+__global__ __launch_bounds__(BLOCK) void k_texture_lookup(SceneView S, const double* uv, int64_t n, double* rgb,
+                                                         uint32_t* flags) {
+    uint32_t err = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        const d3 c = tex_rgb(S, 0, uv[i], uv[n + i], err);
+        rgb[i] = c.x;
+        rgb[n + i] = c.y;
+        rgb[2 * n + i] = c.z;
+    }
+    if (err) atomicOr(flags, err);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_primary_rays(srt_camera cam, const double* J, int64_t n, double* O,
@@ -966,6 +1098,8 @@ struct FrameSlot {
     // frame buffers
     double* fb = nullptr;
     int64_t fb_cap = 0;
+    unsigned long long* fbx = nullptr;  // [3][npix] fixed-point sums (fb_add)
+    int64_t fbx_cap = 0;
     double* rgb = nullptr;
     int64_t rgb_cap = 0;
     uint8_t* u8 = nullptr;
@@ -1058,6 +1192,10 @@ struct srt_ctx {
     int nslots = 4;
     bool use_mt_stream = false;
     bool use_copy_stream = false;
+    // option "deterministic" (default 1): contributions added to a pixel by other threads go into
+    // order-independent fixed-point sums (bit-reproducible frames); 0: f64 atomics
+    bool deterministic = true;
+    bool fx_ok = true;  // cleared when a contribution left the fixed-point range (until the next scene)
     FrameSlot* f = &slots[0];
     bool pipeline = false;  // option "pipeline": size every slot on every frame (no first-use allocation)
     int next_slot = 0;      // slot of the next asynchronous frame
@@ -1348,6 +1486,7 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S, uint32_t* retry 
         bits |= hp[F.cnt_words + 1];
     }
     if (bits & RETRY_CHAIN_TIE) c->chain_ok = false;  // no chain mode for this scene any more
+    if (bits & RETRY_FIXED_RANGE) c->fx_ok = false;   // f64 atomics for this scene
     if (retry) *retry = bits;
     if (bits) return SRT_RETRY;
     double ms_trace = 0.0, ms_primary = 0.0;
@@ -1416,7 +1555,7 @@ void free_slot(FrameSlot& f) {
     (void)hipStreamSynchronize(f.stream);
     free_list(f.queue_bufs);
     free_list(f.ring_bufs);
-    void* bufs[] = {f.fb, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb,
+    void* bufs[] = {f.fb, f.fbx, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb,
                     f.mt_win};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -1478,8 +1617,9 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     c->f = &c->slots[0];
     if (first_err) return first_err;
     if (overflow)
-        return fail(SRT_ERR_MEMORY, "a ray queue overflowed (queues grown) or a tie met chain mode (chain mode "
-                                    "off) during an asynchronous frame: render that frame again");
+        return fail(SRT_ERR_MEMORY, "a ray queue overflowed (queues grown), a tie met chain mode (chain mode "
+                                    "off) or a colour left the fixed-point range (f64 sums from now on) during an "
+                                    "asynchronous frame: render that frame again");
     c->async_stats = last;
     if (st) *st = last;
     return SRT_OK;
@@ -1606,6 +1746,13 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
+    if (!strcmp(key, "deterministic")) {
+        HIP_TRY(hipSetDevice(c->device));
+        int rc = finish_async(c, nullptr);
+        if (rc) return rc;
+        c->deterministic = value != 0;
+        return SRT_OK;
+    }
     if (!strcmp(key, "rehearse_shard")) {
         // diagnostic: act as rank (value & 255) of (value >> 8) ranks without a communicator, so one
         // GPU can render the shards of an N-rank frame in turn (no gather; SRT_RENDER_RGB_ROWS still
@@ -1758,6 +1905,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     c->chain_ok = true;
     c->hint_key[0] = -1;  // ray counts of another scene are no plan for this one
     c->has_scene = true;
+    c->fx_ok = true;
     return SRT_OK;
 }
 
@@ -1863,7 +2011,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     if (async && c->async_pending > 0) {
         const FramePlan& pp = c->f->pending ? c->f->plan : c->slots[c->last_slot].plan;
         const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && n_rows <= c->cam_cap[2] &&
-                          3 * npix <= c->f->fb_cap && 3 * npix <= c->f->rgb_cap && 3 * npix <= c->f->u8_cap &&
+                          3 * npix <= c->f->fb_cap && 3 * npix <= c->f->fbx_cap && 3 * npix <= c->f->rgb_cap &&
+                          3 * npix <= c->f->u8_cap &&
                           jit_doubles <= c->f->jit_cap &&
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
                           (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
@@ -1900,6 +2049,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         c->f = &fs;
         int r = SRT_OK;
         if (!r) r = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * npix);
+        if (!r) r = ensure_buf(&c->f->fbx, c->f->fbx_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
@@ -1997,6 +2147,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             const int64_t nrays = (int64_t)ns * npix;
             TraceParams P = base_params(c, a->seed);
             P.fb = c->f->fb;
+            P.fbx = (c->deterministic && c->fx_ok) ? c->f->fbx : nullptr;
             P.fb_first = (p == 0);  // the first pass's depth-0 kernel stores the framebuffer (no memset)
             // samples per k_primary thread: all of the pass's (accumulated in registers) unless the
             // frame has fewer pixels than a quarter of the resident wave slots, then fewer (pixel x
@@ -2007,7 +2158,11 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             {
                 const int64_t want_items = (int64_t)c->max_blocks * 64;
                 while (P.spt > 1 && npix * ((ns + P.spt - 1) / P.spt) < want_items) P.spt = (P.spt + 1) / 2;
-                if (P.spt < ns && p == 0) HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * npix * 8, c->f->stream));
+                if (P.spt < ns && p == 0) {
+                    HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * npix * 8, c->f->stream));
+                    if (c->deterministic && c->fx_ok)
+                        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)3 * npix * 8, c->f->stream));
+                }
             }
             P.npix = npix;
             P.cam = *cam;
@@ -2136,6 +2291,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         uint32_t* hlast = c->f->host + (F.npass - 1) * F.pass_words;
         if (c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
         hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
+                           (F.frame || !c->deterministic || !c->fx_ok) ? nullptr
+                                                                       : (const unsigned long long*)c->f->fbx,
                            fused ? (int64_t)0 : npix, c->f->shadow, hshadow, (double)a->spp, res_rgb, res_u8, c->f->counts,
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
@@ -2258,7 +2415,12 @@ int srt_stream(srt_ctx* c, void** stream) {
     return SRT_OK;
 }
 
-int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
+}  // extern "C"
+
+namespace {
+// get_raycolor (srt_trace) or Material.get_color at given hits (srt_shade: fid/ft/fo non-null)
+int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const double* ft, const double* fo,
+               srt_stats* st) {
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !a || !a->origin || !a->dir || !a->out_rgb) return fail(SRT_ERR_ARG, "null argument");
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
@@ -2279,16 +2441,29 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
     HIP_TRY(hipMemcpyAsync(O, a->origin, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
     HIP_TRY(hipMemcpyAsync(D, a->dir, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
     if (med) HIP_TRY(hipMemcpyAsync(med, a->medium, (size_t)n * 4, hipMemcpyDefault, c->f->stream));
+    int32_t* dfid = nullptr;
+    double *dft = nullptr, *dfo = nullptr;
+    if (fid) {
+        HIP_TRY(dalloc(&dfid, n));
+        HIP_TRY(dalloc(&dft, n));
+        HIP_TRY(dalloc(&dfo, n));
+        HIP_TRY(hipMemcpyAsync(dfid, fid, (size_t)n * 4, hipMemcpyDefault, c->f->stream));
+        HIP_TRY(hipMemcpyAsync(dft, ft, (size_t)n * 8, hipMemcpyDefault, c->f->stream));
+        HIP_TRY(hipMemcpyAsync(dfo, fo, (size_t)n * 8, hipMemcpyDefault, c->f->stream));
+    }
     if ((rc = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * n))) return rc;
+    if ((rc = ensure_buf(&c->f->fbx, c->f->fbx_cap, 3 * n))) return rc;
     if ((rc = ensure_queues(c, n * c->fanout))) return rc;
     // depths a->depth .. a->depth + cap (the batch's depth is a scalar in the reference)
     const int d0 = a->depth;
     const int dlast = std::min(SRT_MAX_DEPTHS - 2, d0 + depth_cap(c));
     srt_stats S{};
     std::vector<uint32_t> counts(SRT_MAX_DEPTHS * NSHARD);
+    bool fx = c->deterministic;  // fixed-point colour sums (fb_add)
     for (int attempt = 0;; ++attempt) {
         if (attempt > 8) { rc = fail(SRT_ERR_MEMORY, "ray queues keep overflowing"); break; }
         HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * n * 8, c->f->stream));
+        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)3 * n * 8, c->f->stream));
         HIP_TRY(hipMemsetAsync(c->f->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->f->stream));
         HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
         HIP_TRY(hipMemsetAsync(c->f->shadow, 0, 8 * NSHARD, c->f->stream));
@@ -2301,6 +2476,7 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
         HIP_TRY(hipGetLastError());
         TraceParams P = base_params(c, a->seed);
         P.fb = c->f->fb;
+        P.fbx = fx ? c->f->fbx : nullptr;
         P.npix = n;
         const Variant& V = pick_variant(c->mats);
         for (int d = d0; d <= dlast; ++d) {
@@ -2309,7 +2485,17 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
             P.qout = c->f->q[(d + 1) & 1];
             P.cnt_in = c->f->counts + (int64_t)d * NSHARD;
             P.cnt_out = c->f->counts + (int64_t)(d + 1) * NSHARD;
-            hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream, P);
+            if (fid && d == d0) {
+                P.force_id = dfid;
+                P.force_t = dft;
+                P.force_o = dfo;
+                hipLaunchKernelGGL((c->mats & MAT_BVH) ? k_shade_forced<MAT_ALL | MAT_BVH> : k_shade_forced<MAT_ALL>,
+                                   dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream, P);
+                P.force_id = nullptr;
+                P.force_t = P.force_o = nullptr;
+            } else {
+                hipLaunchKernelGGL(V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream, P);
+            }
             HIP_TRY(hipGetLastError());
         }
         uint32_t flags[2];
@@ -2321,7 +2507,8 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
         if ((rc = check_flags(flags[0]))) break;
         if (flags[1]) {
             S.retries++;
-            if ((rc = ensure_queues(c, 2 * c->f->seg * NSHARD))) break;
+            if (flags[1] & RETRY_FIXED_RANGE) fx = false;  // again with f64 atomics
+            if ((flags[1] & RETRY_OVERFLOW) && (rc = ensure_queues(c, 2 * c->f->seg * NSHARD))) break;
             continue;
         }
         if (depth_total(counts.data() + (int64_t)(dlast + 1) * NSHARD, c->f->seg) != 0) {
@@ -2332,16 +2519,36 @@ int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
         S.n_depths = dlast + 1;
         for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.total_rays += S.rays_per_depth[d];
         S.shadow_rays = (int64_t)shadow;
-        HIP_TRY(hipMemcpy(a->out_rgb, c->f->fb, (size_t)3 * n * 8, hipMemcpyDefault));
+        hipLaunchKernelGGL(k_fx_combine, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
+                           (const unsigned long long*)c->f->fbx, n);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->fb, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
+        HIP_TRY(hipStreamSynchronize(c->f->stream));
         break;
     }
     (void)hipFree(O);
     (void)hipFree(D);
     if (med) (void)hipFree(med);
+    void* fb_[] = {dfid, dft, dfo};
+    for (void* b : fb_)
+        if (b) (void)hipFree(b);
     if (rc) return rc;
     S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     if (st) *st = S;
     return SRT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int srt_trace(srt_ctx* c, const srt_trace_args* a, srt_stats* st) {
+    return trace_impl(c, a, nullptr, nullptr, nullptr, st);
+}
+
+int srt_shade(srt_ctx* c, const srt_trace_args* a, const int32_t* collider, const double* t, const double* orient,
+              srt_stats* st) {
+    if (!collider || !t || !orient) return fail(SRT_ERR_ARG, "null hit arrays");
+    return trace_impl(c, a, collider, t, orient, st);
 }
 
 int srt_nearest(srt_ctx* c, const double* O, const double* D, int64_t n, double* t, int32_t* id, double* orient) {
@@ -2395,6 +2602,72 @@ int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O,
     (void)hipFree(dD);
     (void)hipFree(dout);
     return SRT_OK;
+}
+
+int srt_collider_surface(srt_ctx* c, const srt_collider* col, const double* P, int64_t n, double* N, double* uv,
+                         int primitive_uv) {
+    if (!c || !col || !P || (!N && !uv)) return fail(SRT_ERR_ARG, "null argument");
+    if (col->type < 0 || col->type > 3) return fail(SRT_ERR_ARG, "bad collider type");
+    if (uv && col->type == SRT_TRIANGLE)
+        return fail(SRT_ERR_ARG, "Triangle uv is undefined in the reference (triangle.py:79-83)");
+    if (n <= 0) return SRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    srt_collider rec = *col;
+    if (!primitive_uv) rec.flags &= ~SRT_CF_UV_CROSS;  // the collider's own 4x3 cross coordinates
+    double *dP, *dN = nullptr, *duv = nullptr;
+    srt_collider* dcol;
+    HIP_TRY(dalloc(&dP, 3 * n));
+    if (N) HIP_TRY(dalloc(&dN, 3 * n));
+    if (uv) HIP_TRY(dalloc(&duv, 2 * n));
+    HIP_TRY(dalloc(&dcol, 1));
+    HIP_TRY(hipMemcpy(dP, P, (size_t)3 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dcol, &rec, sizeof(srt_collider), hipMemcpyDefault));
+    hipLaunchKernelGGL(k_collider_surface, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, dcol, dP, n,
+                       dN, duv);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
+    if (N) HIP_TRY(hipMemcpy(N, dN, (size_t)3 * n * 8, hipMemcpyDefault));
+    if (uv) HIP_TRY(hipMemcpy(uv, duv, (size_t)2 * n * 8, hipMemcpyDefault));
+    void* bufs[] = {dcol, dP, dN, duv};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    return SRT_OK;
+}
+
+int srt_texture_lookup(srt_ctx* c, const srt_texture* tex, const uint8_t* texels, int64_t texel_bytes,
+                       const double* uv, int64_t n, double* rgb) {
+    if (!c || !tex || !texels || !uv || !rgb) return fail(SRT_ERR_ARG, "null argument");
+    if (tex->offset < 0 || tex->offset + tex->height * tex->width * tex->channels > texel_bytes)
+        return fail(SRT_ERR_ARG, "texture record outside the texel array");
+    if (n <= 0) return SRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    uint8_t* dtexels;
+    srt_texture* dtex;
+    double *duv, *drgb;
+    uint32_t* dflags;
+    HIP_TRY(dalloc(&dtexels, texel_bytes));
+    HIP_TRY(dalloc(&dtex, 1));
+    HIP_TRY(dalloc(&duv, 2 * n));
+    HIP_TRY(dalloc(&drgb, 3 * n));
+    HIP_TRY(dalloc(&dflags, 1));
+    HIP_TRY(hipMemcpy(dtexels, texels, (size_t)texel_bytes, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dtex, tex, sizeof(srt_texture), hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(duv, uv, (size_t)2 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemset(dflags, 0, 4));
+    SceneView S{};
+    S.tex = (const RT_RO srt_texture*)dtex;
+    S.texels = (const RT_RO uint8_t*)dtexels;
+    S.ntex = 1;
+    hipLaunchKernelGGL(k_texture_lookup, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, S, duv, n, drgb,
+                       dflags);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
+    uint32_t flags = 0;
+    HIP_TRY(hipMemcpy(&flags, dflags, 4, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(rgb, drgb, (size_t)3 * n * 8, hipMemcpyDefault));
+    void* bufs[] = {dtexels, dtex, duv, drgb, dflags};
+    for (void* b : bufs) (void)hipFree(b);
+    return check_flags(flags);
 }
 
 int srt_primary_rays(srt_ctx* c, const srt_camera* cam, const double* J, double* O, double* D) {

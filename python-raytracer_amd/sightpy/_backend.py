@@ -239,8 +239,10 @@ def _media_of(ray_n, count):
     return [tuple(complex(v) for v in row) for row in uniq], inv.reshape(-1).astype(np.int32)
 
 
-def trace_rays(ray, scene, seed=None, return_stats=False):
-    """get_raycolor(ray, scene) on the device: colour of every ray of the batch."""
+def trace_rays(ray, scene, seed=None, return_stats=False, hits=None):
+    """get_raycolor(ray, scene) on the device: colour of every ray of the batch.  `hits`:
+    (collider index per ray, distance, orientation) -- Material.get_color at those hits
+    (srt_shade) instead of the nearest-hit search of the first depth."""
     lib, ctx = context()
     n = len(ray)
     uniq, inv = _media_of(ray.n, n)
@@ -258,7 +260,13 @@ def trace_rays(ray, scene, seed=None, return_stats=False):
     a.seed = int(seed if seed is not None else _default_seed()) & (2**64 - 1)
     a.out_rgb = N.ptr(out)
     st = N.Stats()
-    N.check(lib, lib.srt_trace(ctx, ctypes.byref(a), ctypes.byref(st)))
+    if hits is None:
+        N.check(lib, lib.srt_trace(ctx, ctypes.byref(a), ctypes.byref(st)))
+    else:
+        ids = np.ascontiguousarray(np.broadcast_to(np.asarray(hits[0], dtype=np.int32), (n,)))
+        t = np.ascontiguousarray(np.broadcast_to(np.asarray(hits[1], dtype=np.float64), (n,)))
+        o = np.ascontiguousarray(np.broadcast_to(np.asarray(hits[2], dtype=np.float64), (n,)))
+        N.check(lib, lib.srt_shade(ctx, ctypes.byref(a), N.ptr(ids), N.ptr(t), N.ptr(o), ctypes.byref(st)))
     col = vec3(out[0], out[1], out[2])
     return (col, st.as_dict()) if return_stats else col
 
@@ -286,6 +294,37 @@ def intersect_collider(collider, O, D):
     Da = _planar(D, n)
     out = np.empty((2, n))
     N.check(lib, lib.srt_intersect_collider(ctx, N.ptr(rec.reshape(1)), N.ptr(Oa), N.ptr(Da), n, N.ptr(out)))
+    return out
+
+
+def collider_surface(collider, P, normal=True, uv=True, primitive_uv=False):
+    """Collider.get_Normal (3, n) and get_uv (2, n) at points P on the device
+    (srt_collider_surface); `primitive_uv` applies the owning Cuboid/SkyBox's (4, 3) divide."""
+    lib, ctx = context()
+    rec = np.ascontiguousarray(collider_record(collider))
+    if getattr(getattr(collider, "assigned_primitive", None), "uv_cube_cross", False):
+        rec["flags"] |= N.CF_UV_CROSS
+    Pa = _planar(P)
+    n = Pa.shape[1]
+    Nout = np.empty((3, n)) if normal else None
+    uvout = np.empty((2, n)) if uv else None
+    N.check(lib, lib.srt_collider_surface(ctx, N.ptr(rec.reshape(1)), N.ptr(Pa), n, N.ptr(Nout), N.ptr(uvout),
+                                          int(bool(primitive_uv))))
+    return Nout, uvout
+
+
+def texture_lookup(u8, repeat, u, v, linear=True):
+    """image.get_color at (u, v) on the device (srt_texture_lookup): rgb (3, n)."""
+    from ._lower import texture_record
+
+    lib, ctx = context()
+    rec, texels = texture_record(u8, repeat, linear)
+    uv = np.ascontiguousarray(np.stack(np.broadcast_arrays(np.asarray(u, dtype=np.float64),
+                                                           np.asarray(v, dtype=np.float64))).reshape(2, -1))
+    n = uv.shape[1]
+    out = np.empty((3, n))
+    N.check(lib, lib.srt_texture_lookup(ctx, N.ptr(rec.reshape(1)), N.ptr(texels), texels.size, N.ptr(uv), n,
+                                        N.ptr(out)))
     return out
 
 

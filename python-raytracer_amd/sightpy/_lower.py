@@ -184,6 +184,14 @@ def _medium_f0(n_ray, n_mat):
     return out
 
 
+def texture_record(u8, repeat=1.0, linear=True):
+    """One srt_texture record over its own texel array (offset 0): image.get_color's lookup
+    (srt_texture_lookup).  `linear`: the load_image_as_linear_sRGB table, else load_image's."""
+    pool = _TexturePool()
+    i = pool.add(u8, _LIN_LUT if linear else _RAW_LUT, repeat=repeat)
+    return pool.records[i], np.ascontiguousarray(np.concatenate([im.reshape(-1) for im in pool.images]))
+
+
 def collider_record(c):
     """One srt_collider record (no material/primitive fields)."""
     rec = np.zeros((), dtype=N.COLLIDER_DTYPE)

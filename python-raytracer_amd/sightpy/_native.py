@@ -224,6 +224,9 @@ SIGNATURES = {
     "srt_trace": (ctypes.c_int, [_p, ctypes.POINTER(TraceArgs), ctypes.POINTER(Stats)]),
     "srt_nearest": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, _p, _p]),
     "srt_intersect_collider": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int64, _p]),
+    "srt_shade": (ctypes.c_int, [_p, ctypes.POINTER(TraceArgs), _p, _p, _p, ctypes.POINTER(Stats)]),
+    "srt_collider_surface": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, _p, ctypes.c_int]),
+    "srt_texture_lookup": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, ctypes.c_int64, _p]),
     "srt_primary_rays": (ctypes.c_int, [_p, ctypes.POINTER(CameraDesc), _p, _p, _p]),
     "srt_mt19937_uniforms": (ctypes.c_int, [_p, _p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, _p, _p,
                                             ctypes.POINTER(ctypes.c_int32)]),

@@ -43,5 +43,11 @@ class Primitive:
         for c in self.collider_list:
             c.rotate(M, self.center)
 
+    uv_cube_cross = False  # Cuboid / SkyBox: the cube-cross texture layout (cuboid.py:29-32)
+
     def get_uv(self, hit):
-        return hit.collider.get_uv(hit)
+        """Texture coordinates of the hit (sphere.py:17, plane.py:34, cuboid.py:29-32)."""
+        u, v = hit.collider.get_uv(hit)
+        if self.uv_cube_cross:
+            u, v = u / 4, v / 3
+        return u, v

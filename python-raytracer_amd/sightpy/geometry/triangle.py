@@ -43,3 +43,7 @@ class Triangle_Collider(Collider):
         self.n23 = self.n23.matmul(M)
         self.normal = self.normal.matmul(M)
         self.centroid = center + (self.centroid - center).matmul(M)
+
+    def get_uv(self, hit):
+        # triangle.py:79-83 reads pu/pv/w/h, which a Triangle_Collider never has
+        raise NotImplementedError("Triangle uv is undefined in the reference (triangle.py:79-83)")

@@ -1,9 +1,11 @@
 """Material base class (reference `materials/material.py:11-44`).
 
 A material here is a parameter record.  Its `get_color(scene, ray, hit)` — the reference's
-per-batch shading entry point — runs on the device: the shading kernels in
-`csrc/rt_device.h` (`rt_shade_*`) implement each subclass.  Normal maps (material.py:18-40) are
-supported for Plane and Cuboid colliders (the only ones with `inverse_basis_matrix`).
+per-batch shading entry point — runs on the device (`srt_shade`): the shading kernels in
+`csrc/rt_device.h` (`rt_shade_*`) implement each subclass, and the reflected / refracted /
+diffuse rays a hit spawns are traced to completion as in get_raycolor.  Normal maps
+(material.py:18-40) are supported for Plane and Cuboid colliders (the only ones with
+`inverse_basis_matrix`).
 """
 from ..utils.image_functions import load_image_u8
 
@@ -23,7 +25,19 @@ class Material:
         self.normalmap = self.normalmap_u8 / 256.0
         self.repeat = repeat
 
+    def get_Normal(self, hit):
+        """Shading normal (material.py:18-36).  Normal-mapped materials shade on the device only."""
+        if self.normalmap is not None:
+            raise NotImplementedError("normal-mapped shading normals are evaluated inside srt_shade / srt_render")
+        return hit.collider.get_Normal(hit) * hit.orientation
+
     def get_color(self, scene, ray, hit):
-        raise NotImplementedError(
-            "%s shading runs on the device; trace rays with sightpy.get_raycolor" % type(self).__name__
-        )
+        """Colour of the batch `ray` at `hit` (all rays hit `hit.collider` at `hit.distance` with
+        `hit.orientation`), as get_raycolor adds it (ray.py:131-146): srt_shade on the device."""
+        from .._backend import trace_rays
+
+        if hit.collider.assigned_primitive.material is not self:
+            raise ValueError("a hit is shaded by the material of its collider's primitive")
+        ids = scene.collider_list.index(hit.collider)
+        hit.point = ray.origin + ray.dir * hit.distance
+        return trace_rays(ray, scene, hits=(ids, hit.distance, hit.orientation))

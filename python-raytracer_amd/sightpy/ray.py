@@ -74,6 +74,17 @@ class Hit:
         self.N = None
         self.point = None
 
+    def get_uv(self):
+        if self.u is None:  # computed once per hit (ray.py:111-114)
+            self.u, self.v = self.collider.assigned_primitive.get_uv(self)
+        return self.u, self.v
+
+    def get_normal(self):
+        # ray.py:116-119 calls collider.get_N, which no collider defines; get_Normal is meant
+        if self.N is None:
+            self.N = self.collider.get_Normal(self)
+        return self.N
+
 
 def get_raycolor(ray, scene):
     """Colour of every ray of the batch (reference ray.py:122-148), traced on the GPU."""

@@ -110,9 +110,8 @@ def test_scene_render_device_stream_equals_host_stream():
     np.random.seed(5)
     b = np.asarray(sc.render(2, rng="numpy-host"))
     sb = np.random.get_state()
-    # same jitter; the framebuffer's depth >= 1 atomics may round a u8 differently
-    d = np.abs(a.astype(int) - b.astype(int))
-    assert d.max() <= 1 and (d > 0).mean() < 1e-3
+    # same jitter, and the framebuffer sums are order-independent: the same image
+    assert np.array_equal(a, b)
     assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
 
 
