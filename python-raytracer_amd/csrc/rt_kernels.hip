@@ -188,6 +188,18 @@ __device__ __forceinline__ double fx_value(const unsigned long long* fbx, int64_
     return (double)(long long)fbx[ch * npix + p] * FX_UNIT;
 }
 
+// a pixel-channel sum the resolve must not trust: negative (no material of the reference adds a
+// negative term, so a wrapped sum of non-negative terms) or >= 2^18 (half the range: the sum grew
+// towards the wrap).  A sum that wrapped twice (a pixel-channel total >= 2^20) is not detectable.
+__device__ __forceinline__ bool fx_suspect(const unsigned long long* fbx, int64_t npix, int64_t p) {
+    bool bad = false;
+    for (int ch = 0; ch < 3; ++ch) {
+        const long long v = (long long)fbx[ch * npix + p];
+        bad |= (v < 0) | (v >= (1ll << 62));
+    }
+    return bad;
+}
+
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -901,6 +913,7 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, const unsig
                 r += fx_value(fbx, npix, 0, p);
                 g += fx_value(fbx, npix, 1, p);
                 b += fx_value(fbx, npix, 2, p);
+                if (fx_suspect(fbx, npix, p)) shadow_host[2] = RETRY_FIXED_RANGE;  // render again with f64
             }
             r /= spp;
             g /= spp;
@@ -914,9 +927,14 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, const unsig
 }
 
 // fb += the fixed-point sums (srt_trace's colours)
-__global__ __launch_bounds__(BLOCK) void k_fx_combine(double* fb, const unsigned long long* fbx, int64_t npix) {
-    for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK)
+__global__ __launch_bounds__(BLOCK) void k_fx_combine(double* fb, const unsigned long long* fbx, int64_t npix,
+                                                     uint32_t* flags) {
+    bool bad = false;
+    for (int64_t p = (int64_t)blockIdx.x * BLOCK + threadIdx.x; p < npix; p += (int64_t)gridDim.x * BLOCK) {
         for (int ch = 0; ch < 3; ++ch) fb[ch * npix + p] += fx_value(fbx, npix, ch, p);
+        bad |= fx_suspect(fbx, npix, p);
+    }
+    if (bad) atomicOr(flags + 1, RETRY_FIXED_RANGE);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O, const double* D, int64_t n, double* t,
@@ -1485,6 +1503,7 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S, uint32_t* retry 
         if ((rc = check_flags(hp[F.cnt_words]))) return rc;
         bits |= hp[F.cnt_words + 1];
     }
+    bits |= c->f->host[F.npass * F.pass_words + 2];
     if (bits & RETRY_CHAIN_TIE) c->chain_ok = false;  // no chain mode for this scene any more
     if (bits & RETRY_FIXED_RANGE) c->fx_ok = false;   // f64 atomics for this scene
     if (retry) *retry = bits;
@@ -1533,6 +1552,7 @@ void clear_host_flags(srt_ctx* c, const FramePlan& F) {
         c->f->host[p * F.pass_words + F.cnt_words] = 0u;
         c->f->host[p * F.pass_words + F.cnt_words + 1] = 0u;
     }
+    c->f->host[F.npass * F.pass_words + 2] = 0u;  // k_resolve's fixed-point range check
 }
 
 // Stream and counters of a slot, created on first use.
@@ -2070,15 +2090,15 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         }
         // per-pass counters and flags come back through pinned memory once, at the end of the
         // frame: the passes, the resolve and the output copies are queued without a host round trip
-        if (!r && c->f->host_words < F.npass * F.pass_words + 2) {
+        if (!r && c->f->host_words < F.npass * F.pass_words + 3) {
             if (c->f->host) (void)hipHostFree(c->f->host);
             c->f->host = nullptr;
             c->f->host_words = 0;
-            if (hipHostMalloc((void**)&c->f->host, (size_t)(F.npass * F.pass_words + 2) * 4, hipHostMallocDefault) !=
+            if (hipHostMalloc((void**)&c->f->host, (size_t)(F.npass * F.pass_words + 3) * 4, hipHostMallocDefault) !=
                 hipSuccess) {
                 r = fail(SRT_ERR_MEMORY, "pinned host allocation failed");
             } else {
-                c->f->host_words = F.npass * F.pass_words + 2;
+                c->f->host_words = F.npass * F.pass_words + 3;  // + shadow count (2), resolve's fx check
                 memset(c->f->host, 0, (size_t)c->f->host_words * 4);  // depths beyond used_words stay zero
             }
         }
@@ -2519,9 +2539,18 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
         S.n_depths = dlast + 1;
         for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.total_rays += S.rays_per_depth[d];
         S.shadow_rays = (int64_t)shadow;
-        hipLaunchKernelGGL(k_fx_combine, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
-                           (const unsigned long long*)c->f->fbx, n);
-        HIP_TRY(hipGetLastError());
+        if (fx) {
+            hipLaunchKernelGGL(k_fx_combine, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
+                               (const unsigned long long*)c->f->fbx, n, c->f->flags);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(flags, c->f->flags, sizeof(flags), hipMemcpyDeviceToHost, c->f->stream));
+            HIP_TRY(hipStreamSynchronize(c->f->stream));
+            if (flags[1] & RETRY_FIXED_RANGE) {
+                S.retries++;
+                fx = false;  // again with f64 atomics
+                continue;
+            }
+        }
         HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->fb, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
         HIP_TRY(hipStreamSynchronize(c->f->stream));
         break;

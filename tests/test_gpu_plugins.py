@@ -84,7 +84,9 @@ def test_gpu_cube_cross_primitive_uv():
 
     c.assigned_primitive = CrossPrim()
     ru, rv = O.collider_uv(c, P)
-    _, uv = _backend().collider_surface(c, P, normal=False, primitive_uv=True)
+    from sightpy import vec3
+
+    _, uv = _backend().collider_surface(c, vec3(*P), normal=False, primitive_uv=True)
     np.testing.assert_allclose(uv[0], ru / 4, rtol=FTOL, atol=1e-15)
     np.testing.assert_allclose(uv[1], rv / 3, rtol=FTOL, atol=1e-15)
     h = _Hit(c, P).h
@@ -100,7 +102,7 @@ def test_gpu_triangle_uv_is_undefined_like_reference():
     with pytest.raises(NotImplementedError):
         c.get_uv(_Hit(c, P).h)
     with pytest.raises(_native.SrtError):  # the C ABI refuses it as well
-        _backend().collider_surface(c, P, normal=False)
+        _backend().collider_surface(c, _Hit(c, P).h.point, normal=False)
 
 
 def test_gpu_texture_lookup_matches_oracle():
@@ -124,7 +126,14 @@ def test_gpu_image_get_color_at_hits():
     from sightpy.textures.texture import image
     from sightpy.utils.colour_functions import sRGB_to_sRGB_linear
 
+    from sightpy.geometry.primitive import Primitive
+
+    class PlanePrim:
+        uv_cube_cross = False
+        get_uv = Primitive.get_uv
+
     c, P = _kat_points("plane_tilted")
+    c.assigned_primitive = PlanePrim()
     tex = image.__new__(image)
     tex.u8 = np.random.default_rng(9).integers(0, 256, (16, 24, 3), dtype=np.uint8)
     tex.repeat = 2.0
