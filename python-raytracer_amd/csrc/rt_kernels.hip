@@ -24,7 +24,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_bvh.h"
@@ -830,13 +832,16 @@ struct Variant {
     void (*frame)(TraceParams);
     void (*chain)(TraceParams);
 };
-// occupancy experiments for the headline scene (srt_set_option "occupancy" = 1 (index 2), 3, 4);
-// the default instantiations use 2 waves/SIMD, the fastest measured (profiles/)
+// occupancy experiments for the headline scene (srt_set_option "occupancy" = 1 (index 2), 3, 4;
+// built with -DRT_OCC_VARIANTS, tools/build_ablations.sh); the default instantiations use
+// 2 waves/SIMD, the fastest measured (profiles/)
+#ifdef RT_OCC_VARIANTS
 const Variant OCC_VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>, k_frame<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1, true>},
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>, k_frame<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3, true>},
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>, k_frame<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4, true>},
 };
+#endif
 int g_occupancy = 0;
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>, k_frame<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY, 2, true>},
@@ -849,7 +854,9 @@ const Variant VARIANTS[] = {
      k_trace<MAT_ALL | MAT_BVH, 2, true>},
 };
 const Variant& pick_variant(uint32_t mats) {
+#ifdef RT_OCC_VARIANTS
     if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
+#endif
     for (const Variant& v : VARIANTS)
         if ((v.mats & mats) == mats) return v;
     return VARIANTS[sizeof(VARIANTS) / sizeof(VARIANTS[0]) - 1];
@@ -1103,6 +1110,7 @@ struct FrameSlot {
     hipEvent_t jit_free = nullptr;   // recorded on `stream` after the last kernel that reads the jitter
     bool jit_busy = false;           // `jit_free` guards the jitter buffer
     uint32_t* mt_win = nullptr;      // segment windows of this slot's numpy-stream generation
+    int64_t mt_win_cap = 0;
     // ray queues: 2 x NSHARD segments of `seg` rays
     Queue q[2]{};
     int64_t seg = 0;
@@ -1182,9 +1190,22 @@ struct srt_ctx {
     int64_t cam_cap[3] = {0, 0, 0};
     std::vector<uint8_t> cam_host[3];  // host copies of what xs / ys / rows hold
     uint32_t* mt = nullptr;    // MT19937 jump tables (255 x 624), two round keys, two final windows
-    // frame-end jump polynomial of the last pipelined frame shape (rt_mt.h xpow_mod / end_jump)
-    int64_t mt_end_words = -1;
-    uint32_t* mt_end_poly = nullptr;
+    // the y words (k_mt_y) of a generation's key: [0] / [1] those of the two final windows (made
+    // by the end block that made the window, valid flag per window), [2] scratch for other keys
+    uint32_t* mt_y = nullptr;
+    bool mt_y_valid[2] = {false, false};
+    // band mode (a shard's rows of the numpy stream, rt_mt_kernel.h MtArgs::bands): per pass shape,
+    // the segment list and its jump polynomials (host-made once, kept for the context's life)
+    struct MtBandTab {
+        int64_t key[5];
+        uint64_t rows_hash;
+        int nseg;
+        int64_t* bands;   // device [nseg][2]
+        uint32_t* polys;  // device [nseg][624]
+    };
+    std::deque<MtBandTab> mt_bandtabs;  // (stable addresses: frames hold pointers into it)
+    std::vector<std::pair<int64_t, uint32_t*>> mt_end_polys;  // frame-end jump polynomial per word count
+    bool mt_bands_on = true;  // option "mt_bands"
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
@@ -1434,6 +1455,129 @@ int mt_ensure(srt_ctx* c) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)MT_LDS_BYTES));
     HIP_TRY(dalloc(&c->mt, MT_NTAB + 4 * rtmt::N));
     HIP_TRY(hipMemcpy(c->mt, rtmt::tables_flat(), MT_NTAB * 4, hipMemcpyHostToDevice));
+    HIP_TRY(dalloc(&c->mt_y, (int64_t)3 * MT_YBLOCKS * rtmt::N));
+    return SRT_OK;
+}
+
+uint32_t* mt_dump_at(srt_ctx* c, int d) { return c->mt + MT_NTAB + (2 + d) * rtmt::N; }
+uint32_t* mt_ybuf(srt_ctx* c, int i) { return c->mt_y + (int64_t)i * MT_YBLOCKS * rtmt::N; }
+
+// The y words of `key` for a generation on `st`: those an end block made with the key (a final
+// window), else k_mt_y into the scratch buffer (one workgroup, ~34 blocks).  Generations of
+// different frames are ordered by the key they hand on, so one scratch buffer suffices.
+const uint32_t* mt_y_for(srt_ctx* c, hipStream_t st, const uint32_t* key) {
+    for (int d = 0; d < 2; ++d)
+        if (key == mt_dump_at(c, d) && c->mt_y_valid[d]) return mt_ybuf(c, d);
+    hipLaunchKernelGGL(k_mt_y, dim3(1), dim3(MT_THREADS), 0, st, key, mt_ybuf(c, 2));
+    return mt_ybuf(c, 2);
+}
+
+// x^end_jump(n_words) mod phi on the device, made once per word count (a few shapes per context)
+int mt_end_poly_for(srt_ctx* c, int64_t n_words, const uint32_t** out) {
+    for (auto& e : c->mt_end_polys)
+        if (e.first == n_words) { *out = e.second; return SRT_OK; }
+    uint32_t* d = nullptr;
+    HIP_TRY(dalloc(&d, rtmt::N));
+    const std::vector<uint32_t> poly = rtmt::xpow_mod(rtmt::end_jump(n_words));
+    HIP_TRY(hipMemcpy(d, poly.data(), rtmt::N * 4, hipMemcpyHostToDevice));
+    c->mt_end_polys.emplace_back(n_words, d);
+    *out = d;
+    return SRT_OK;
+}
+
+// Band mode table of one pass shape: the rows' runs of `ns` samples' stored planes (a run is split
+// at 2^18 doubles so no segment generates more than the tabulated mode's), each with its jump
+// polynomial x^(2 d0 - 1) mod phi (xpow_mod, ~2.5 ms each, over a few host threads).
+constexpr int MT_MAX_BANDS = 2048;
+int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, const int32_t* rows, int n_rows,
+                  const srt_ctx::MtBandTab** out) {
+    uint64_t h = 1469598103934665603ull;
+    for (int k = 0; k < n_rows; ++k) h = (h ^ (uint64_t)(uint32_t)rows[k]) * 1099511628211ull;
+    const int64_t key[5] = {W, Hf, ns, plane_mask, n_rows};
+    for (auto& t : c->mt_bandtabs)
+        if (!memcmp(t.key, key, sizeof key) && t.rows_hash == h) { *out = &t; return SRT_OK; }
+    std::vector<int64_t> segs;
+    for (int s = 0; s < ns; ++s)
+        for (int j = 0; j < 4; ++j) {
+            if (!((plane_mask >> j) & 1)) continue;
+            for (int k = 0; k < n_rows;) {
+                int e = k + 1;
+                while (e < n_rows && rows[e] == rows[e - 1] + 1) ++e;
+                int64_t d0 = ((int64_t)(s * 4 + j) * Hf + rows[k]) * W;
+                int64_t n = (int64_t)(e - k) * W;
+                while (n > 0) {
+                    const int64_t m = std::min<int64_t>(n, (int64_t)1 << 18);
+                    segs.push_back(d0);
+                    segs.push_back(m);
+                    d0 += m;
+                    n -= m;
+                }
+                k = e;
+            }
+        }
+    const int nseg = (int)(segs.size() / 2);
+    *out = nullptr;
+    if (nseg > MT_MAX_BANDS || nseg == 0) return SRT_OK;  // (the tabulated segments instead)
+    std::vector<uint32_t> polys((size_t)nseg * rtmt::N, 0u);
+    const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int w = 0; w < nth; ++w)
+        th.emplace_back([&, w] {
+            for (int i = w; i < nseg; i += nth) {
+                if (segs[2 * i] == 0) continue;  // starts from the key
+                const std::vector<uint32_t> p = rtmt::xpow_mod((uint64_t)(2 * segs[2 * i] - 1));
+                std::copy(p.begin(), p.end(), polys.begin() + (size_t)i * rtmt::N);
+            }
+        });
+    for (auto& t : th) t.join();
+    srt_ctx::MtBandTab T{};
+    memcpy(T.key, key, sizeof key);
+    T.rows_hash = h;
+    T.nseg = nseg;
+    HIP_TRY(dalloc(&T.bands, (int64_t)segs.size()));
+    HIP_TRY(dalloc(&T.polys, (int64_t)polys.size()));
+    HIP_TRY(hipMemcpy(T.bands, segs.data(), segs.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(T.polys, polys.data(), polys.size() * 4, hipMemcpyHostToDevice));
+    c->mt_bandtabs.push_back(T);
+    *out = &c->mt_bandtabs.back();
+    return SRT_OK;
+}
+
+// Band mode generation of n_words words from (key, pos): only the table's segments are generated
+// (their doubles at their place in `out`, the whole pass's layout), every one jumped to from the key;
+// the final window (next key) and its y come from the jump kernel's end block.
+int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, int pos, int64_t n_words,
+                    const srt_ctx::MtBandTab& T, double* out, int* final_pos, const uint32_t* end_poly,
+                    hipEvent_t key_ready) {
+    const int64_t abs_end = pos + n_words;
+    const int64_t dump_abs = ((abs_end + rtmt::N - 1) / rtmt::N - 1) * rtmt::N;
+    MtArgs A{};
+    A.key = key;
+    A.tab = T.polys;
+    A.bands = T.bands;
+    A.out = out;
+    A.words = n_words;
+    A.double_base = 0;
+    A.n_out = INT64_MAX;
+    A.pos = pos;
+    A.dump_at = dump_abs;
+    A.dump_dst = mt_dump_at(c, c->mt_cur ^ 1);
+    A.end_poly = end_poly;
+    A.end_at = (int64_t)rtmt::end_jump(n_words);
+    A.key_in_win = 1;
+    A.y = mt_y_for(c, st, key);
+    A.y_next = mt_ybuf(c, c->mt_cur ^ 1);
+    hipLaunchKernelGGL(k_mt_jump, dim3(T.nseg + 1), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
+    HIP_TRY(hipGetLastError());
+    if (key_ready) HIP_TRY(hipEventRecord(key_ready, st));
+    MtArgs G = A;
+    G.dump_dst = nullptr;
+    G.y_next = nullptr;
+    hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, st, G, (const uint32_t*)win);
+    HIP_TRY(hipGetLastError());
+    c->mt_y_valid[c->mt_cur ^ 1] = true;
+    c->mt_cur ^= 1;
+    *final_pos = (int)(abs_end - dump_abs);
     return SRT_OK;
 }
 
@@ -1475,12 +1619,18 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
         }
         const int jump_blocks = (R.nseg - 1) + (end ? 1 : 0);
         A.key_in_win = jump_blocks > 0;
+        if (A.dump_dst) {
+            A.y_next = end ? mt_ybuf(c, c->mt_cur ^ 1) : nullptr;
+            c->mt_y_valid[c->mt_cur ^ 1] = end;  // (a generator segment makes the window, not its y)
+        }
         if (jump_blocks > 0) {
+            A.y = mt_y_for(c, st, A.key);
             hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
             HIP_TRY(hipGetLastError());
         }
         if (end && key_ready) HIP_TRY(hipEventRecord(key_ready, st));
         MtArgs G = A;
+        G.y_next = nullptr;
         if (end) G.dump_dst = nullptr;  // (made by the jump kernel)
         hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, G, (const uint32_t*)win);
         HIP_TRY(hipGetLastError());
@@ -1750,9 +1900,14 @@ int srt_destroy(srt_ctx* c) {
     if (c->mt_done) (void)hipEventDestroy(c->mt_done);
     if (c->mt_stream) (void)hipStreamDestroy(c->mt_stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_end_poly};
+    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_y};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    for (auto& t : c->mt_bandtabs) {
+        (void)hipFree(t.bands);
+        (void)hipFree(t.polys);
+    }
+    for (auto& e : c->mt_end_polys) (void)hipFree(e.second);
     delete c;
     return SRT_OK;
 }
@@ -1763,6 +1918,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
@@ -2024,6 +2180,19 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if ((rc = ensure_slot(f))) return rc;
         c->f = &f;
     }
+    // numpy stream of a shard (rows not the whole frame): band mode, only the rows' runs generated
+    // (rt_mt_kernel.h MtArgs::bands); tables for the full passes and the last pass
+    const int mt_pm = cam->lens_radius != 0.0 ? 15 : 3;  // a pinhole camera reads planes 0 and 1 only
+    const srt_ctx::MtBandTab* mt_bt[2] = {nullptr, nullptr};
+    int64_t mt_win_need = (int64_t)rtmt::SEGS * rtmt::N;
+    if (use_mt && c->mt_bands_on && n_rows < Hf) {
+        const int last_ns = a->spp - (F.npass - 1) * batch;
+        for (int k = 0; k < 2; ++k) {
+            if ((rc = mt_band_table(c, W, Hf, k == 0 ? batch : last_ns, mt_pm, rows_src, n_rows, &mt_bt[k]))) return rc;
+            if (mt_bt[k]) mt_win_need = std::max(mt_win_need, (int64_t)(mt_bt[k]->nseg + 1) * rtmt::N);
+        }
+        if (!mt_bt[0] || !mt_bt[1]) mt_bt[0] = mt_bt[1] = nullptr;
+    }
     const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * W * Hf : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
     const int64_t maxpix = sharded ? (int64_t)band_rows(Hf, c->nranks, 0).size() * W : 0;  // rank 0 has the most rows
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
@@ -2033,7 +2202,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && n_rows <= c->cam_cap[2] &&
                           3 * npix <= c->f->fb_cap && 3 * npix <= c->f->fbx_cap && 3 * npix <= c->f->rgb_cap &&
                           3 * npix <= c->f->u8_cap &&
-                          jit_doubles <= c->f->jit_cap &&
+                          jit_doubles <= c->f->jit_cap && (!use_mt || mt_win_need <= c->f->mt_win_cap) &&
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
                           (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
                           F.frame == pp.frame && F.chain_from == pp.chain_from && F.W == pp.W && F.H == pp.H &&
@@ -2073,6 +2242,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
+        if (!r && use_mt) r = ensure_buf(&c->f->mt_win, c->f->mt_win_cap, mt_win_need);
         if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
         if (!r && sharded && c->rank == 0) {
             r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, c->nranks * maxpix * 3);
@@ -2198,24 +2368,25 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 const int64_t n_out = (int64_t)ns * 4 * W * Hf;
                 const int64_t n_skip = (p + 1 == F.npass) ? 4 * W * Hf : 0;
                 if (p > 0) mt_key = mt_dump(c);  // the previous pass's final window
-                if (!c->f->mt_win && dalloc(&c->f->mt_win, (int64_t)rtmt::SEGS * rtmt::N) != hipSuccess)
-                    return fail(SRT_ERR_MEMORY, "window table allocation failed");
                 // a pipelined one-pass frame: its final window (the next frame's key) by one jump, so
                 // the next frame's generation starts once this one's jump kernel has run
                 const int64_t n_words = 2 * (n_out + n_skip);
-                const bool end = async && F.npass == 1 && n_words <= (int64_t)rtmt::SEGS * rtmt::L &&
-                                 rtmt::end_jump(n_words) > 0;
-                if (end && c->mt_end_words != n_words) {
-                    if (!c->mt_end_poly) HIP_TRY(dalloc(&c->mt_end_poly, rtmt::N));
-                    const std::vector<uint32_t> poly = rtmt::xpow_mod(rtmt::end_jump(n_words));
-                    HIP_TRY(hipMemcpy(c->mt_end_poly, poly.data(), rtmt::N * 4, hipMemcpyHostToDevice));
-                    c->mt_end_words = n_words;
-                }
+                const srt_ctx::MtBandTab* bt = mt_bt[p + 1 == F.npass ? 1 : 0];
+                const bool band = bt && rtmt::end_jump(n_words) > 0;
+                const bool end = band || (async && F.npass == 1 && n_words <= (int64_t)rtmt::SEGS * rtmt::L &&
+                                          rtmt::end_jump(n_words) > 0);
+                const uint32_t* end_poly = nullptr;
+                if (end && (rc = mt_end_poly_for(c, n_words, &end_poly))) return rc;
                 // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
-                if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos, W * Hf,
-                                    cam->lens_radius != 0.0 ? 15 : 3, end ? c->mt_end_poly : nullptr,
-                                    end ? (int64_t)rtmt::end_jump(n_words) : 0, end ? c->mt_done : nullptr)))
+                if (band) {
+                    if ((rc = mt_launch_bands(c, mst, c->f->mt_win, mt_key, mt_pos, n_words, *bt, c->f->jit, &mt_pos,
+                                              end_poly, p + 1 == F.npass ? c->mt_done : nullptr)))
+                        return rc;
+                } else if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos,
+                                           W * Hf, mt_pm, end_poly, end ? (int64_t)rtmt::end_jump(n_words) : 0,
+                                           end ? c->mt_done : nullptr))) {
                     return rc;
+                }
                 // otherwise the next frame's stream may start as soon as this one's is generated
                 if (p + 1 == F.npass && !end) HIP_TRY(hipEventRecord(c->mt_done, mst));
                 if (mst != c->f->stream) {
@@ -2769,8 +2940,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     hipStream_t st = c->f->stream;
     HIP_TRY(hipMemcpyAsync(mt_key0(c), key, rtmt::N * 4, hipMemcpyHostToDevice, st));
     int final_pos = 0;
-    if (!c->f->mt_win && dalloc(&c->f->mt_win, (int64_t)rtmt::SEGS * rtmt::N) != hipSuccess)
-        return fail(SRT_ERR_MEMORY, "window table allocation failed");
+    if ((rc = ensure_buf(&c->f->mt_win, c->f->mt_win_cap, (int64_t)rtmt::SEGS * rtmt::N))) return rc;
     if ((rc = mt_launch(c, st, c->f->mt_win, mt_key0(c), pos, n_out, n_skip, dst, &final_pos))) return rc;
     if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(key_out, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost, st));

@@ -145,10 +145,13 @@ struct Gf2 {
 };
 
 inline const std::vector<int>& phi_terms() {  // exponents e < 19937 of phi's terms
-    static std::vector<int> t;
-    if (t.empty())
+    // (a magic static: initialised once even when several host threads make polynomials)
+    static const std::vector<int> t = [] {
+        std::vector<int> v;
         for (int i = 0; i < POLY_BITS; ++i)
-            if ((RT_MT_PHI[i >> 5] >> (i & 31)) & 1u) t.push_back(i);
+            if ((RT_MT_PHI[i >> 5] >> (i & 31)) & 1u) v.push_back(i);
+        return v;
+    }();
     return t;
 }
 

@@ -28,29 +28,40 @@ struct MtArgs {
     int64_t end_at;            // window position of that jump
     int32_t key_in_win;        // the key window is copied to win[0] by k_mt_jump (segment 0 reads it there)
     int32_t pad_;
+    // y: the MT_YBLOCKS x 624 raw words generated from the key window (k_mt_y, or the previous
+    // frame's end block), read by every jump block instead of each block generating them itself
+    const uint32_t* y;
+    uint32_t* y_next;     // end block: the y of the final window (the next frame's key), or null
+    // band mode (a shard's rows): segment s stores bands[2 s + 1] doubles from double bands[2 s] of
+    // the call (one band of rows of one jitter plane), jumped to by tab[s] = x^(2 bands[2 s] - 1) mod
+    // phi (host-made per frame shape); its window is win[s + 1] (win[0]: the key).  Null: the
+    // tabulated 2^19-word segments.
+    const int64_t* bands;
 };
 
-// Two launches per round.
-//  k_mt_jump: one workgroup per segment s >= 1 that has anything to store.  y = the 34 x 624 raw words
-//    generated from the key window (LDS), then W'[m] = XOR_{i : p_i} y[i + m] -- wave v takes
-//    coefficient words [78 v, 78 v + 78), lane g the ten outputs m = 10 g .. 10 g + 9 with
-//    y[32 w + 10 g .. + 41] in registers, so a set bit costs ten register XORs and no LDS traffic; the
-//    eight waves' partial windows are XOR-reduced through LDS and written to the window table.
+// Launches per round (k_mt_y only when no earlier end block made the key's y).
+//  k_mt_y: one workgroup: y = the 34 x 624 raw words generated from the key window, to HBM.
+//  k_mt_jump: one workgroup per segment s >= 1 that has anything to store.  y (HBM -> LDS), then
+//    W'[m] = XOR_{i : p_i} y[i + m] -- wave v of 16 takes coefficient words [39 v, 39 v + 39) (scalar
+//    loads), lane g the eleven outputs m = 11 g .. 11 g + 10 with y[32 w + 11 g .. + 42] in registers
+//    (single-word LDS reads: the odd lane stride is free of bank conflicts); each coefficient bit is
+//    one v_bitop3 acc ^= y & mask per output, branch-free; the waves' partial windows are XOR-reduced
+//    through LDS and written to the window table.
 //  k_mt_gen: MT_GEN_THREADS per segment.  A ring of three 624-word blocks in LDS; the next block is
 //    made in three dependent stages of 227 / 227 / 170 words (x_{k+624} = x_{k+397} ^ twist(x_k,
 //    x_{k+1}): stage two and three take their x_{k+397} from the thread's own earlier word) while the
 //    current block's 312 doubles are tempered and stored.  7.5 KB of LDS and five waves per segment:
 //    the trace kernels of the previous frame keep the rest of the CU.
-constexpr int MT_THREADS = 512;
+constexpr int MT_THREADS = 1024;
 constexpr int MT_WAVES = MT_THREADS / 64;
-constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 78 coefficient words
-constexpr int MT_G = 10;                              // window outputs per lane in the jump
+constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 39 coefficient words
+constexpr int MT_G = 11;  // window outputs per lane in the jump (odd: conflict-free LDS reads; 57 lanes cover 624)
 constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
-constexpr int MT_RED = 640;                           // per-wave stride of the reduction buffer
+constexpr int MT_RED = 704;                           // per-wave stride of the reduction buffer (64 x 11)
 static_assert(MT_CW_PER_WAVE * MT_WAVES == rtmt::N, "coefficient words split evenly over the waves");
-static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 42 <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
+static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 32 + MT_G <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
 static_assert(MT_WAVES * MT_RED + 3 * rtmt::N <= MT_YBLOCKS * rtmt::N, "the reduction and end ring alias y");
-constexpr size_t MT_LDS_BYTES = (size_t)(MT_YBLOCKS + 1) * rtmt::N * 4;  // y + coefficient words
+constexpr size_t MT_LDS_BYTES = (size_t)MT_YBLOCKS * rtmt::N * 4;  // y
 // generator threads per segment: 5 waves (227 make the next block, 312 store the current one).
 // Measured (222 segments, ex1 1080p pinhole planes): 1 wave 1.17 ms, 4 waves 0.64, 5 waves 0.50,
 // 8 waves 0.50 -- one wave is VALU-issue bound (~3000 cycles per 624-word block)
@@ -94,6 +105,17 @@ struct MtSeg {
 
 __device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
     MtSeg g;
+    if (A.bands) {
+        const int64_t d0 = A.bands[2 * s];
+        g.ws = d0 == 0 ? 0 : 2 * d0 - 1;
+        g.lo = 2 * d0 + A.pos;
+        g.dbase = A.double_base + d0;
+        g.kend = (int)A.bands[2 * s + 1];
+        g.gen_end = g.lo + 2 * (int64_t)g.kend;
+        g.chain = g.dump = false;
+        g.chain_at = 0;
+        return g;
+    }
     g.ws = rtmt::window_start(s);
     const int64_t end = A.pos + A.words;  // round-relative, exclusive
     g.lo = (int64_t)s * rtmt::L + A.pos;
@@ -117,60 +139,85 @@ __device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
     return g;
 }
 
-// block s - 1 of the grid: the window of segment s >= 1 into win + 624 s.  With A.end_poly the last
-// block instead jumps to the window at A.end_at and generates forward to the final window (A.dump_at),
-// written to A.dump_dst: the next frame's key, ready when this kernel ends (its whole generation need
-// not have run).  Block 0 also copies the key window to win[0] for segment 0's generator.
+// The raw words y = W_0, T W_0, ... (MT_YBLOCKS blocks of 624) from the key window, for the jump
+// blocks of a generation: one workgroup, two LDS blocks ping-ponged.
+__global__ __launch_bounds__(MT_THREADS) void k_mt_y(const uint32_t* key, uint32_t* y) {
+    __shared__ uint32_t buf[2 * rtmt::N];
+    const int t = threadIdx.x;
+    for (int m = t; m < rtmt::N; m += MT_THREADS) buf[m] = y[m] = key[m];
+    __syncthreads();
+    for (int q = 0; q + 1 < MT_YBLOCKS; ++q) {
+        const uint32_t* p = buf + (q & 1) * rtmt::N;
+        uint32_t* n = buf + ((q + 1) & 1) * rtmt::N;
+        mt_next_block(p, n, t);
+        mt_barrier();
+        for (int m = t; m < rtmt::N; m += MT_THREADS) y[(int64_t)(q + 1) * rtmt::N + m] = n[m];
+    }
+}
+
+// Tabulated mode: block s - 1 of the grid makes the window of segment s >= 1 into win + 624 s.  Band
+// mode (A.bands): block s makes segment s's window into win + 624 (s + 1) (none for a band at the
+// call's first double: it starts from the key).  With A.end_poly the last block instead jumps to the
+// window at A.end_at and generates forward to the final window (A.dump_at), written to A.dump_dst --
+// the next frame's key, ready when this kernel ends (its whole generation need not have run) -- and
+// on to the y of that window (A.y_next), so the next frame's jump blocks need no k_mt_y.  Block 0
+// also copies the key window to win[0] for the generators that start from it.
 __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win) {
-    extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words (+ 624 coefficient words)
+    extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words
     uint32_t* y = mt_lds;
-    uint32_t* coef = mt_lds + MT_YBLOCKS * rtmt::N;
     uint32_t* red = mt_lds;                   // MT_WAVES x MT_RED (aliases y once it is read)
     uint32_t* ring = mt_lds + MT_WAVES * MT_RED;  // end block: 3 blocks after the reduction
     const bool end_block = A.end_poly && blockIdx.x == gridDim.x - 1;
-    const int s = blockIdx.x + 1;
+    const bool band = A.bands != nullptr;
+    const int s = band ? (int)blockIdx.x : (int)blockIdx.x + 1;
     const int t = threadIdx.x;
     if (blockIdx.x == 0)
         for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
-    if (!end_block && mt_seg(A, s).idle()) return;
-    const uint32_t* poly = end_block ? A.end_poly : A.tab + (int64_t)(s - 1) * rtmt::N;
-    for (int m = t; m < rtmt::N; m += MT_THREADS) {
-        y[m] = A.key[m];
-        coef[m] = poly[m];
+    if (!end_block && (band ? A.bands[2 * s] == 0 : mt_seg(A, s).idle())) return;
+    const uint32_t* poly = end_block ? A.end_poly : A.tab + (int64_t)(band ? s : s - 1) * rtmt::N;
+    {
+        const uint4* ys = reinterpret_cast<const uint4*>(A.y);
+        uint4* yl = reinterpret_cast<uint4*>(y);
+#ifndef MT_DBG_NOLOAD  // (timing harness only)
+        for (int m = t; m < MT_YBLOCKS * rtmt::N / 4; m += MT_THREADS) yl[m] = ys[m];
+#endif
     }
     __syncthreads();
-    for (int q = 0; q + 1 < MT_YBLOCKS; ++q) {
-        mt_next_block(y + q * rtmt::N, y + (q + 1) * rtmt::N, t);
-        mt_barrier();
-    }
-    const int wv = t >> 6, g = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), g = t & 63;
     uint32_t acc[MT_G];
 #pragma unroll
     for (int k = 0; k < MT_G; ++k) acc[k] = 0u;
-    for (int cw_i = wv * MT_CW_PER_WAVE; cw_i < (wv + 1) * MT_CW_PER_WAVE; ++cw_i) {
-        const uint32_t cw = __builtin_amdgcn_readfirstlane(coef[cw_i]);
+    // per coefficient word: the lane's 43 words of y from LDS, then for each of the 32
+    // bits acc[k] ^= y[32 cw_i + j + 10 g + k] & mask_j in one v_bitop3 (a ^ (b & c)) with the mask
+    // in an SGPR -- branch-free (a uniform branch per bit cost more than the masked half of the ops)
+    // the wave's 39 coefficient words, one per lane, read out per iteration by v_readlane (a load per
+    // iteration exposed its whole latency every time)
+    const uint32_t my_cw = g < MT_CW_PER_WAVE ? poly[wv * MT_CW_PER_WAVE + g] : 0u;
+#ifdef MT_DBG_CW  // (timing harness only: fewer coefficient words per wave)
+    for (int ci = 0; ci < MT_DBG_CW; ++ci) {
+#else
+    for (int ci = 0; ci < MT_CW_PER_WAVE; ++ci) {
+#endif
+        const int cw_i = wv * MT_CW_PER_WAVE + ci;
+        const uint32_t cw = __builtin_amdgcn_readlane(my_cw, ci);
         if (cw == 0u) continue;
-        // y[32 cw_i + 10 g ...]: an even word index, so 8-byte aligned pair loads
-        const uint2* yp = reinterpret_cast<const uint2*>(y + 32 * cw_i + MT_G * g);
+        // y[32 cw_i + 11 g + i]: single-word loads, the odd lane stride keeps them free of bank conflicts
+        const uint32_t* yp = y + 32 * cw_i + MT_G * g;
         uint32_t r[32 + MT_G];
 #pragma unroll
-        for (int k = 0; k < (32 + MT_G) / 2; ++k) {
-            const uint2 v = yp[k];
-            r[2 * k] = v.x;
-            r[2 * k + 1] = v.y;
-        }
+        for (int k = 0; k < 32 + MT_G; ++k) r[k] = yp[k];
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
-            if (cw & (1u << j)) {  // wave-uniform
+            const uint32_t m = 0u - ((cw >> j) & 1u);  // wave-uniform
 #pragma unroll
-                for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + k];
-            }
+            for (int k = 0; k < MT_G; ++k) acc[k] = __builtin_amdgcn_bitop3_b32(acc[k], r[j + k], m, 0x78);
         }
     }
     __syncthreads();  // every wave is done reading y
 #pragma unroll
     for (int k = 0; k < MT_G; ++k) red[wv * MT_RED + MT_G * g + k] = acc[k];
     __syncthreads();
+    uint32_t* wdst = win + (int64_t)(band ? s + 1 : s) * rtmt::N;
     for (int m = t; m < rtmt::N; m += MT_THREADS) {
         uint32_t w = 0u;
 #pragma unroll
@@ -178,19 +225,21 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
         if (end_block)
             ring[m] = w;
         else
-            win[(int64_t)s * rtmt::N + m] = w;
+            wdst[m] = w;
     }
     if (!end_block) return;
-    // end block: generate from the window at end_at until the final window is written
+    // end block: generate from the window at end_at until the final window (and its y) is written
     __syncthreads();
+    const int64_t stop = A.dump_at + (A.y_next ? (int64_t)MT_YBLOCKS * rtmt::N : (int64_t)rtmt::N);
     int slot = 0;
-    for (int64_t b0 = A.end_at; b0 < A.dump_at + rtmt::N; b0 += rtmt::N) {
+    for (int64_t b0 = A.end_at; b0 < stop; b0 += rtmt::N) {
         const uint32_t* cur = ring + slot * rtmt::N;
         const int next = slot == 2 ? 0 : slot + 1;
-        if (b0 + rtmt::N < A.dump_at + rtmt::N) mt_next_block(cur, ring + next * rtmt::N, t);
+        if (b0 + rtmt::N < stop) mt_next_block(cur, ring + next * rtmt::N, t);
         for (int m = t; m < rtmt::N; m += MT_THREADS) {
-            const int64_t x = b0 + m;
-            if (x >= A.dump_at && x < A.dump_at + rtmt::N) A.dump_dst[x - A.dump_at] = cur[m];
+            const int64_t x = b0 + m - A.dump_at;
+            if (x >= 0 && x < rtmt::N) A.dump_dst[x] = cur[m];
+            if (A.y_next && x >= 0 && x < (int64_t)MT_YBLOCKS * rtmt::N) A.y_next[x] = cur[m];
         }
         slot = next;
         mt_barrier();
@@ -207,7 +256,8 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
     const int lane = threadIdx.x;
     const MtSeg g = mt_seg(A, s);
     if (g.idle()) return;
-    const uint32_t* w0p = (s == 0 && !A.key_in_win) ? A.key : win + (int64_t)s * rtmt::N;
+    const uint32_t* w0p = A.bands ? (g.ws == 0 ? win : win + (int64_t)(s + 1) * rtmt::N)
+                                  : (s == 0 && !A.key_in_win) ? A.key : win + (int64_t)s * rtmt::N;
     for (int m = lane; m < rtmt::N; m += NT) ring[m] = w0p[m];
     __syncthreads();
     // block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it holds

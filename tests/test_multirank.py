@@ -284,3 +284,96 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world):
     finally:
         lib.srt_set_option(ctx, b"rehearse_shard", 0)
         lib.srt_host_free(ctx, host)
+
+
+def _set_option(key, value):
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    N.check(lib, lib.srt_set_option(ctx, key.encode(), int(value)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["multipass", "thin_lens", "odd_rows"])
+def test_gpu_band_mode_stream_equals_tabulated_stream(case):
+    """A shard's numpy stream in band mode (only its rows' runs generated, each jumped to from the
+    key by a host-made polynomial; rt_mt_kernel.h MtArgs::bands) against the tabulated 2^19-word
+    segments (option mt_bands=0), through several passes (full and last-pass band tables), a thin-lens
+    camera (all four planes stored) and an arbitrary row set; numpy's state advances identically."""
+    import scenes
+    from sightpy import _backend as B
+    from sightpy._shard import shard_rows
+
+    W, H = 96, 72
+    sc = scenes.example1(W, H, 3)
+    spp, batch, rows = 2, None, shard_rows(H, 4, 1)
+    if case == "multipass":
+        spp, batch = 5, 2
+    elif case == "thin_lens":
+        sc.camera.lens_radius = 0.05
+    else:
+        rows = np.array([0, 1, 2, 9, 10, 33, 50, 51, 52, 53, 71])
+    out, states = {}, {}
+    try:
+        for bands in (0, 1):
+            _set_option("mt_bands", bands)
+            np.random.seed(33)
+            out[bands] = B.render_scene(sc, spp, seed=5, mt=True, rows=rows, batch_size=batch)
+            states[bands] = np.random.get_state()
+    finally:
+        _set_option("mt_bands", 1)
+    assert np.array_equal(out[0].rgb, out[1].rgb)
+    assert np.array_equal(out[0].srgb8, out[1].srgb8)
+    assert states[0][2] == states[1][2] and np.array_equal(states[0][1], states[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_gpu_async_band_mode_shard_frames_match_sync_frames(world):
+    """Pipelined frames of one rank's shard (the multi-GPU bench loop, rehearsed on one card): in band
+    mode each frame's key and its y words come from the previous frame's end block; every frame equals
+    the synchronous shard render from the same numpy state, and the state after the sequence matches."""
+    import ctypes
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+    from sightpy._shard import shard_rows
+
+    W, H, K, spp = 160, 96, 5, 2
+    sc = scenes.example1(W, H, 4)
+    rows = shard_rows(H, world, world - 1)
+    np.random.seed(9)
+    ref = [B.render_scene(sc, spp, seed=5, mt=True, rows=rows) for _ in range(K)]
+    want = np.random.get_state()
+    lib, ctx = B.context()
+    np.random.seed(9)
+    mt = N.MtState.from_numpy()
+    B.upload(sc)
+    cd = B.camera_desc(sc.camera)
+    hosts = []
+    try:
+        for k in range(K):
+            h = ctypes.c_void_p()
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * W * H * 8, ctypes.byref(h)))
+            hosts.append(h)
+        N.check(lib, lib.srt_set_option(ctx, b"rehearse_shard", (world << 8) | (world - 1)))
+        a = N.RenderArgs()
+        a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, H, 0
+        a.jitter, a.seed, a.out_hit_id, a.rows, a.out_srgb8 = None, 5, None, None, None
+        a.mt = ctypes.pointer(mt)
+        a.flags = N.RENDER_ASYNC | N.RENDER_SHARDED | N.RENDER_RGB_ROWS
+        for k in range(K):
+            a.out_rgb = hosts[k]
+            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+        N.check(lib, lib.srt_render_finish(ctx, None))
+        mt.to_numpy()
+        got = np.random.get_state()
+        assert got[2] == want[2] and np.array_equal(got[1], want[1])
+        for k in range(K):
+            frame = np.ctypeslib.as_array((ctypes.c_double * (3 * W * H)).from_address(hosts[k].value))
+            mine = frame.reshape(3, H, W)[:, rows].reshape(3, -1)
+            assert np.array_equal(mine, ref[k].rgb), "frame %d" % k
+    finally:
+        lib.srt_set_option(ctx, b"rehearse_shard", 0)
+        for h in hosts:
+            lib.srt_host_free(ctx, h)

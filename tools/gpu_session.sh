@@ -31,10 +31,12 @@ for step in "$@"; do
     pmc_list) run pmc_list 120 rocprofv3 -L ;;
     pmc_sq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_sq1 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
             run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    mttests) run mttests 600 python3 -u -m pytest tests/test_multirank.py tests/test_mt.py tests/test_gpu.py -x -v -m gpu -k "band or shard or mt or numpy_stream or async" --timeout 300 --timeout-method thread -rf ;;
     mctests) run mctests 600 python3 -u -m pytest tests/test_gpu_mc.py -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
     mt) run mt 300 python3 tools/mt_timing.py ;;
     api) run api 300 python3 tools/api_timing.py --repeats 5 --profile ;;
     api_prof) run api_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/api_prof -o api --output-format csv -- python3 tools/api_timing.py --repeats 5 ;;
+    shardprof) run shardprof_${SHARD:-8} 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/shardprof_${SHARD:-8} -o s --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-secondary --shard-of ${SHARD:-8} ;;
     rngdev) run bench_rngdev 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --rng device ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
