@@ -42,8 +42,8 @@ struct MtArgs {
 // Launches per round (k_mt_y only when no earlier end block made the key's y).
 //  k_mt_y: one workgroup: y = the 34 x 624 raw words generated from the key window, to HBM.
 //  k_mt_jump: one workgroup per segment s >= 1 that has anything to store.  y (HBM -> LDS), then
-//    W'[m] = XOR_{i : p_i} y[i + m] -- wave v of 16 takes coefficient words [39 v, 39 v + 39) (scalar
-//    loads), lane g the eleven outputs m = 11 g .. 11 g + 10 with y[32 w + 11 g .. + 42] in registers
+//    W'[m] = XOR_{i : p_i} y[i + m] -- wave v of 16 takes coefficient words [39 v, 39 v + 39) (held
+//    one per lane, read out by v_readlane), lane g the eleven outputs m = 11 g .. 11 g + 10 with y[32 w + 11 g .. + 42] in registers
 //    (single-word LDS reads: the odd lane stride is free of bank conflicts); each coefficient bit is
 //    one v_bitop3 acc ^= y & mask per output, branch-free; the waves' partial windows are XOR-reduced
 //    through LDS and written to the window table.
@@ -52,6 +52,8 @@ struct MtArgs {
 //    x_{k+1}): stage two and three take their x_{k+397} from the thread's own earlier word) while the
 //    current block's 312 doubles are tempered and stored.  7.5 KB of LDS and five waves per segment:
 //    the trace kernels of the previous frame keep the rest of the CU.
+// 16 waves (same-box A/B, ex1 1080p pipelined frames: 1024 threads 1.766 ms/frame, 512 threads
+// 1.80-1.88; one jump block alone 74 vs 111 us)
 constexpr int MT_THREADS = 1024;
 constexpr int MT_WAVES = MT_THREADS / 64;
 constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 39 coefficient words
@@ -187,30 +189,46 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     uint32_t acc[MT_G];
 #pragma unroll
     for (int k = 0; k < MT_G; ++k) acc[k] = 0u;
-    // per coefficient word: the lane's 43 words of y from LDS, then for each of the 32
-    // bits acc[k] ^= y[32 cw_i + j + 10 g + k] & mask_j in one v_bitop3 (a ^ (b & c)) with the mask
-    // in an SGPR -- branch-free (a uniform branch per bit cost more than the masked half of the ops)
-    // the wave's 39 coefficient words, one per lane, read out per iteration by v_readlane (a load per
-    // iteration exposed its whole latency every time)
-    const uint32_t my_cw = g < MT_CW_PER_WAVE ? poly[wv * MT_CW_PER_WAVE + g] : 0u;
+    // per coefficient word: the lane's 43 words y[32 cw_i + 11 g + i] from LDS, then every set bit j
+    // adds y[32 cw_i + j + 11 g + k] to the lane's eleven outputs k.  The wave's 39 coefficient words
+    // are held one per lane and read out by v_readlane.
+    uint32_t my_cw[(MT_CW_PER_WAVE + 63) / 64];
+#pragma unroll
+    for (int h = 0; h < (MT_CW_PER_WAVE + 63) / 64; ++h)
+        my_cw[h] = 64 * h + g < MT_CW_PER_WAVE ? poly[wv * MT_CW_PER_WAVE + 64 * h + g] : 0u;
 #ifdef MT_DBG_CW  // (timing harness only: fewer coefficient words per wave)
     for (int ci = 0; ci < MT_DBG_CW; ++ci) {
 #else
     for (int ci = 0; ci < MT_CW_PER_WAVE; ++ci) {
 #endif
         const int cw_i = wv * MT_CW_PER_WAVE + ci;
-        const uint32_t cw = __builtin_amdgcn_readlane(my_cw, ci);
+        const uint32_t cw = __builtin_amdgcn_readlane(my_cw[ci >> 6], ci & 63);
         if (cw == 0u) continue;
         // y[32 cw_i + 11 g + i]: single-word loads, the odd lane stride keeps them free of bank conflicts
         const uint32_t* yp = y + 32 * cw_i + MT_G * g;
         uint32_t r[32 + MT_G];
 #pragma unroll
         for (int k = 0; k < 32 + MT_G; ++k) r[k] = yp[k];
+        // bit pairs: pattern 01 / 10 adds one shifted row, 11 the pre-XORed pair row d (one XOR per
+        // output either way; a uniform branch per pair).  Measured per jump block (tools/
+        // mt_jump_bench.cpp, 204 bands): pairs 74 us; a v_bitop3 acc ^= y & mask per bit, branch-free,
+        // 117 us; a uniform branch per bit 108 us; nibbles (xor3 of two pair rows) 172 us
+        uint32_t d[32 + MT_G - 1];
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const uint32_t m = 0u - ((cw >> j) & 1u);  // wave-uniform
+        for (int k = 0; k < 32 + MT_G - 1; ++k) d[k] = r[k] ^ r[k + 1];
 #pragma unroll
-            for (int k = 0; k < MT_G; ++k) acc[k] = __builtin_amdgcn_bitop3_b32(acc[k], r[j + k], m, 0x78);
+        for (int j = 0; j < 32; j += 2) {
+            const uint32_t pat = (cw >> j) & 3u;  // wave-uniform
+            if (pat == 1u) {
+#pragma unroll
+                for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + k];
+            } else if (pat == 2u) {
+#pragma unroll
+                for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + 1 + k];
+            } else if (pat == 3u) {
+#pragma unroll
+                for (int k = 0; k < MT_G; ++k) acc[k] ^= d[j + k];
+            }
         }
     }
     __syncthreads();  // every wave is done reading y

@@ -21,9 +21,9 @@ for step in "$@"; do
   case $step in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 900 python3 -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
-    bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
+    bench) run bench 600 python3 bench.py ;;
     bench_nocpu) run bench_nocpu 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
-    shard8) for n in 2 4 8; do run "bench_shard$n" 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --shard-of $n; done ;;
+    shard8) for n in 2 4 8; do run "bench_shard$n" 300 python3 bench.py --no-cpu-baseline --shard-of $n; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write_${CONFIG:-example1_1080p_d5} 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_${CONFIG:-example1_1080p_d5} -o bench --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 3 --warmup 1 --no-cpu-baseline ;;
