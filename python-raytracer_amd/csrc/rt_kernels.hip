@@ -1229,7 +1229,10 @@ struct srt_ctx {
     // shard of an 8-GPU frame (bench --shard-of 8, same box): 3 slots 0.627, 4 slots 0.544, 3 slots +
     // MT stream 0.857.  Four slots (a stream each, HIP's default of four hardware queues per process)
     int nslots = 4;
-    bool use_mt_stream = false;
+    // -1 auto: a high-priority stream of its own for whole frames (ex1 1080p 1.80 -> 1.64 ms/frame,
+    // same box), the frame's stream for a shard (one rank of 8: 0.344 vs 0.381 ms); 0 the frame's
+    // stream; 1 a stream of its own; 2 a high-priority one
+    int use_mt_stream = -1;
     bool use_copy_stream = false;
     // option "deterministic" (default 1): contributions added to a pixel by other threads go into
     // order-independent fixed-point sums (bit-reproducible frames); 0: f64 atomics
@@ -1952,7 +1955,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
             c->nslots = (int)value;
             c->next_slot = 0;
         } else if (!strcmp(key, "mt_stream")) {
-            c->use_mt_stream = value != 0;
+            c->use_mt_stream = (int)std::min<int64_t>(std::max<int64_t>(value, -1), 2);
+            if (c->mt_stream) {
+                (void)hipStreamDestroy(c->mt_stream);
+                c->mt_stream = nullptr;
+            }
         } else {
             c->use_copy_stream = value != 0;
         }
@@ -2314,8 +2321,17 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         // (it waits until the slot's previous frame has read its jitter), else the frame's stream
         hipStream_t mst = c->f->stream;
         if (use_mt) {
-            if (F.npass == 1 && c->use_mt_stream) {
-                if (!c->mt_stream) HIP_TRY(hipStreamCreateWithFlags(&c->mt_stream, hipStreamNonBlocking));
+            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream : (n_rows < Hf ? 0 : 2);
+            if (F.npass == 1 && mts) {
+                if (!c->mt_stream) {
+                    // a high-priority queue (mt_stream 2): the generation's blocks are dispatched ahead
+                    // of the trace kernels' as CUs free up
+                    int lo = 0, hi = 0;
+                    if (mts == 2 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+                        HIP_TRY(hipStreamCreateWithPriority(&c->mt_stream, hipStreamNonBlocking, hi));
+                    else
+                        HIP_TRY(hipStreamCreateWithFlags(&c->mt_stream, hipStreamNonBlocking));
+                }
                 mst = c->mt_stream;
                 if (c->f->jit_busy) HIP_TRY(hipStreamWaitEvent(mst, c->f->jit_free, 0));
             }
@@ -3079,6 +3095,8 @@ int srt_comm_barrier(srt_ctx* c) {
     return srt_comm_allreduce(c, &v, 1, 0);
 }
 
+// (hipHostMalloc places the buffer on the GPU's NUMA node: tools/pcie_probe.py, 56 GB/s either way
+// the calling process is pinned)
 int srt_host_alloc(srt_ctx* c, int64_t bytes, void** out) {
     if (!c || !out || bytes <= 0) return fail(SRT_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));

@@ -42,7 +42,7 @@ struct MtArgs {
 // Launches per round (k_mt_y only when no earlier end block made the key's y).
 //  k_mt_y: one workgroup: y = the 34 x 624 raw words generated from the key window, to HBM.
 //  k_mt_jump: one workgroup per segment s >= 1 that has anything to store.  y (HBM -> LDS), then
-//    W'[m] = XOR_{i : p_i} y[i + m] -- wave v of 16 takes coefficient words [39 v, 39 v + 39) (held
+//    W'[m] = XOR_{i : p_i} y[i + m] -- wave v of 8 takes coefficient words [78 v, 78 v + 78) (held
 //    one per lane, read out by v_readlane), lane g the eleven outputs m = 11 g .. 11 g + 10 with y[32 w + 11 g .. + 42] in registers
 //    (single-word LDS reads: the odd lane stride is free of bank conflicts); each coefficient bit is
 //    one v_bitop3 acc ^= y & mask per output, branch-free; the waves' partial windows are XOR-reduced
@@ -52,11 +52,19 @@ struct MtArgs {
 //    x_{k+1}): stage two and three take their x_{k+397} from the thread's own earlier word) while the
 //    current block's 312 doubles are tempered and stored.  7.5 KB of LDS and five waves per segment:
 //    the trace kernels of the previous frame keep the rest of the CU.
-// 16 waves (same-box A/B, ex1 1080p pipelined frames: 1024 threads 1.766 ms/frame, 512 threads
-// 1.80-1.88; one jump block alone 74 vs 111 us)
-constexpr int MT_THREADS = 1024;
+// 8 waves.  A jump block alone takes 111 us (16 waves: 74 us), but it must find room next to the
+// trace kernels of the frames in flight: a 16-wave block needs more registers per SIMD than one
+// finished trace block frees and waited up to 2.5 ms for whole CUs to drain.  Same box, ex1 1080p
+// pipelined frames, ms/frame (3 x 100 frames): 8 waves + high-priority generation stream 1.64,
+// 16 waves 1.70, 8 waves 1.80, 16 waves + high-priority stream 1.85; one rank of 8 (3 x 400 frames,
+// generation on the frame's stream): 8 waves 0.344, 16 waves 0.355 (tools/_gpu_cmd.sh A/B runs).
+#ifdef MT_THREADS_OVERRIDE  // (experiments)
+constexpr int MT_THREADS = MT_THREADS_OVERRIDE;
+#else
+constexpr int MT_THREADS = 512;
+#endif
 constexpr int MT_WAVES = MT_THREADS / 64;
-constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 39 coefficient words
+constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 78 coefficient words (8 waves)
 constexpr int MT_G = 11;  // window outputs per lane in the jump (odd: conflict-free LDS reads; 57 lanes cover 624)
 constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
 constexpr int MT_RED = 704;                           // per-wave stride of the reduction buffer (64 x 11)

@@ -30,6 +30,11 @@ def main():
     dev, host = ctypes.c_void_p(), ctypes.c_void_p()
     N.check(lib, lib.srt_device_alloc(ctx, n, ctypes.byref(dev)))
     N.check(lib, lib.srt_host_alloc(ctx, n, ctypes.byref(host)))
+    # NUMA node of the buffer's first page (move_pages query)
+    libc = ctypes.CDLL(None, use_errno=True)
+    pages = (ctypes.c_void_p * 1)(host.value)
+    status = (ctypes.c_int * 1)(-99)
+    libc.syscall(279, 0, 1, pages, None, status, 0)
     for _ in range(3):
         N.check(lib, lib.srt_memcpy(ctx, host, dev, n))
     ts = []
@@ -49,8 +54,8 @@ def main():
             lo, _, hi = part.partition("-")
             if lo and int(lo) <= cpu <= int(hi or lo):
                 node = int(d.rsplit("node", 1)[1])
-    print("D2H pinned %d MB: median %.2f GB/s (best %.2f); cpu %d on node %d; GPU numa nodes %s; affinity %d cpus"
-          % (mb, n / ts[len(ts) // 2] / 1e9, n / ts[0] / 1e9, cpu, node, gpu_numa_nodes()[:8],
+    print("D2H pinned %d MB: median %.2f GB/s (best %.2f); buffer on node %d; cpu %d on node %d; GPU numa nodes %s; "
+          "affinity %d cpus" % (mb, n / ts[len(ts) // 2] / 1e9, n / ts[0] / 1e9, status[0], cpu, node, gpu_numa_nodes()[:8],
              len(os.sched_getaffinity(0))), flush=True)
     lib.srt_host_free(ctx, host)
     lib.srt_device_free(ctx, dev)
