@@ -327,41 +327,50 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     }
     RT_ACC(1, tn0);
     if (hit_slot && active) *hit_slot = id;
-    const Em& em = em0;
 #ifdef RT_ABL_NOSHADE  // diagnostic build only: raygen + nearest hit, no shading
-    if (id == 12345) em.local(d3{t, o, 0.0});
+    if (id == 12345) em0.local(d3{t, o, 0.0});
     return;
 #endif
     // waterfall over the colliders hit in this wave: inside each pass the collider index, and so
     // its material and every table entry they reference, is wave-uniform (scalar loads into SGPRs,
     // uniform branches); a wave usually sees one to three distinct colliders
+    // Exact ties (ray.py:131-146: every collider at the nearest distance is shaded and the colours
+    // added) go through the same waterfall: after shading its collider a tied lane moves on to the
+    // next collider (in index order) hit at the same distance, with the next emission round.  One
+    // copy of the shaders per kernel (a separate tie loop held a second one: the kernels waited on
+    // instruction fetch ~10 % of their wave cycles, SQ_WAIT_INST_ANY).
     RT_T0(tw0);
-    uint64_t pending = __ballot(id >= 0);
+    int cur = id;     // collider this lane shades next (-1: done)
+    double co = o;    // its orientation
+    uint32_t rnd = 0;  // emission round: 0 the nearest collider, k the k-th tied one
+    uint64_t pending = __ballot(cur >= 0);
     while (pending) {
         RT_ACC(12, tw0);  // counts waterfall passes (k = 12 calls)
         const int lead = __builtin_ctzll(pending);
-        const int cu = __builtin_amdgcn_readfirstlane(__shfl(id, lead));
-        const bool mine = (id == cu);
+        const int cu = __builtin_amdgcn_readfirstlane(__shfl(cur, lead));
+        const bool mine = (cur == cu);
         if (mine) {
-            // re-derive the uniform index inside the branch: here id == cu on every active lane, and
+            // re-derive the uniform index inside the branch: here cur == cu on every active lane, and
             // the compiler would otherwise substitute the per-lane id back into every table
             // address (vector loads into VGPRs instead of scalar loads)
-            const int cs = __builtin_amdgcn_readfirstlane(id);
+            const int cs = __builtin_amdgcn_readfirstlane(cur);
             const auto& c = S.col[cs];
             const int m = c.material;
+            Em em = em0;
+            if (rnd) em.round = rnd;
             switch (S.mat[m].type) {
                 case SRT_GLOSSY:
-                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<(MATS & MAT_BVH) != 0>(S, c, m, r, t, o, em, err);
+                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<(MATS & MAT_BVH) != 0>(S, c, m, r, t, co, em, err);
                     break;
                 case SRT_REFRACTIVE:
                     if (MATS & mat_bit(SRT_REFRACTIVE))
-                        shade_refractive(S, c, m, r, t, o, em, err, mc_uniform(P, r, cs, 0));
+                        shade_refractive(S, c, m, r, t, co, em, err, mc_uniform(P, r, cs, rnd));
                     break;
                 case SRT_THINFILM:
-                    if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, m, r, t, o, em, err);
+                    if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, m, r, t, co, em, err);
                     break;
                 case SRT_DIFFUSE:
-                    if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse(S, c, m, r, t, o, em, err);
+                    if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse(S, c, m, r, t, co, em, err);
                     break;
                 case SRT_EMISSIVE:
                     if (MATS & mat_bit(SRT_EMISSIVE)) shade_emissive(S, c, m, r, t, em, err);
@@ -371,22 +380,29 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
                     break;
             }
         }
-        pending &= ~__ballot(mine);
+        if (!FORCED && __ballot(mine && ties)) {
+            // the lanes just shaded find their next tied collider: a wave-uniform collider loop
+            // (scalar table loads) from cu + 1
+            int nxt = -1;
+            double no = FARAWAY;
+            for (int c = cu + 1; c < S.ncol; ++c) {
+                double oc;
+                if (mine && ties && nxt < 0 && collider_hit(S.col[c], r.o, r.d, oc) == t) {
+                    nxt = c;
+                    no = oc;
+                }
+            }
+            if (mine) {
+                cur = nxt;
+                co = no;
+                ++rnd;
+            }
+        } else if (mine) {
+            cur = -1;
+        }
+        pending = __ballot(cur >= 0);
     }
     RT_ACC(2, tw0);
-    // colliders tied at the same distance are all shaded and their colours added (ray.py:131-146)
-    if (!FORCED && __ballot(ties)) {
-        // wave-uniform collider loop (scalar table loads); lanes act on later colliders at t
-        uint32_t round = 1;
-        for (int c = 0; c < S.ncol; ++c) {
-            double oc;
-            if (ties && c > id && collider_hit(S.col[c], r.o, r.d, oc) == t) {
-                Em et = em0;
-                et.round = round++;
-                shade_hit<MATS>(S, c, S.col[c].material, r, t, oc, et, err, mc_uniform(P, r, c, round - 1));
-            }
-        }
-    }
 }
 
 // Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
