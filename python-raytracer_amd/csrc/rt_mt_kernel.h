@@ -32,11 +32,14 @@ struct MtArgs {
     // frame's end block), read by every jump block instead of each block generating them itself
     const uint32_t* y;
     uint32_t* y_next;     // end block: the y of the final window (the next frame's key), or null
-    // band mode (a shard's rows): segment s stores bands[2 s + 1] doubles from double bands[2 s] of
-    // the call (one band of rows of one jitter plane), jumped to by tab[s] = x^(2 bands[2 s] - 1) mod
-    // phi (host-made per frame shape); its window is win[s + 1] (win[0]: the key).  Null: the
-    // tabulated 2^19-word segments.
+    // band mode (a shard's rows): segment s covers bands[3 s + 1] doubles from double bands[3 s] of
+    // the call (runs of rows of one jitter plane), jumped to by tab[s] = x^(2 bands[3 s] - 1) mod
+    // phi (host-made per frame shape); its window is win[s + 1] (win[0]: the key).  bands[3 s + 2]
+    // != 0: several runs merged, the segment generates through the other ranks' rows between them
+    // and stores double k only where k % band_period < band_len.  Null: the tabulated 2^19-word
+    // segments.
     const int64_t* bands;
+    int64_t band_len, band_period;
 };
 
 // Launches per round (k_mt_y only when no earlier end block made the key's y).
@@ -110,17 +113,20 @@ struct MtSeg {
     int64_t chain_at;
     int kend;         // pairs [0, kend) are stored (minus the planes outside plane_mask)
     bool chain, dump;
+    bool masked;      // band mode, merged runs: only k % band_period < band_len is stored
     __device__ bool idle() const { return kend == 0 && !chain && !dump; }
 };
 
 __device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
     MtSeg g;
+    g.masked = false;
     if (A.bands) {
-        const int64_t d0 = A.bands[2 * s];
+        const int64_t d0 = A.bands[3 * s];
         g.ws = d0 == 0 ? 0 : 2 * d0 - 1;
         g.lo = 2 * d0 + A.pos;
         g.dbase = A.double_base + d0;
-        g.kend = (int)A.bands[2 * s + 1];
+        g.kend = (int)A.bands[3 * s + 1];
+        g.masked = A.bands[3 * s + 2] != 0;
         g.gen_end = g.lo + 2 * (int64_t)g.kend;
         g.chain = g.dump = false;
         g.chain_at = 0;
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     const int t = threadIdx.x;
     if (blockIdx.x == 0)
         for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
-    if (!end_block && (band ? A.bands[2 * s] == 0 : mt_seg(A, s).idle())) return;
+    if (!end_block && (band ? A.bands[3 * s] == 0 : mt_seg(A, s).idle())) return;
     const uint32_t* poly = end_block ? A.end_poly : A.tab + (int64_t)(band ? s : s - 1) * rtmt::N;
     {
         const uint4* ys = reinterpret_cast<const uint4*>(A.y);
@@ -334,7 +340,8 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
             const int t = lane + NT * i;
             const int k = kq + t;
             if (t < 312 && k >= 0 && k < g.kend &&
-                (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1))) {
+                (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1)) &&
+                (!g.masked || (uint32_t)k % (uint32_t)A.band_period < (uint32_t)A.band_len)) {
                 const int o = off0 + 2 * (c0 + t);  // in-block offset of the pair's first word: -1 .. 622
                 const uint32_t x0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
                 const uint32_t x1 = cur[o + 1];
