@@ -1,8 +1,8 @@
 """End-to-end rate of the public API: `Scene.render(spp)` exactly as an example script calls it
 (scene.py:60-104 here, reference scene.py:71-140): the reference's numpy jitter stream generated on
-the GPU, every sample and depth traced, the linear RGB (f64) and uint8 image copied to host memory
-over PCIe, and the PIL image built.  This is the host-buffer rate DESIGN.md §5 quotes next to
-bench.py's device-resident `value`.
+the GPU, every sample and depth traced, the uint8 image copied to host memory over PCIe (Scene.render
+returns only the PIL image, so the linear RGB stays on the device), and the PIL image built.  Compare
+bench.py, whose frame also brings the linear RGB (f64) to the host.
 
     python tools/api_timing.py [--config example1_1080p_d5] [--repeats 5]
 """
