@@ -271,6 +271,9 @@ def main():
     ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
     ap.add_argument("--option", action="append", default=[],
                     help="experiment: srt_set_option KEY=VALUE before rendering (repeatable)")
+    ap.add_argument("--sync", action="store_true",
+                    help="diagnostic: synchronous timed frames (no pipelining), so a rocprofv3 kernel trace shows each "
+                         "kernel's launch time alone, as the roofline's HIP-event kernel_ms measures it")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job (its per-frame work "
                          "without the gather)")
@@ -363,7 +366,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(async_ok=not args.sync)
     last = N.Stats()
     N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(last)))  # every frame in host memory, flags checked
     if world > 1:
