@@ -1246,7 +1246,7 @@ struct srt_ctx {
     // shard of an 8-GPU frame (bench --shard-of 8, same box): 3 slots 0.627, 4 slots 0.544, 3 slots +
     // MT stream 0.857.  Four slots (a stream each, HIP's default of four hardware queues per process)
     int nslots = 4;
-    // -1 auto: a high-priority stream of its own for frames of at least half the rows (ex1 1080p
+    // -1 auto: a high-priority stream of its own for frames of more than a third of the rows (ex1 1080p
     // 1.80 -> 1.64 ms/frame, same box; one rank of 2: 0.989 -> 0.926 ms), the frame's stream for
     // smaller shards (one rank of 4: 0.581 vs 0.608, of 8: 0.340 vs 0.363); 0 the frame's stream;
     // 1 a stream of its own (0.580 / 0.339: as 0); 2 a high-priority one
@@ -2370,7 +2370,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         // (it waits until the slot's previous frame has read its jitter), else the frame's stream
         hipStream_t mst = c->f->stream;
         if (use_mt) {
-            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream : (2 * (int64_t)n_rows >= Hf ? 2 : 0);
+            // (more than a third of the rows: whole frames and both ranks of a 2-rank frame, whose
+            // shards differ by a band)
+            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream : (3 * (int64_t)n_rows > Hf ? 2 : 0);
             if (F.npass == 1 && mts) {
                 if (!c->mt_stream) {
                     // a high-priority queue (mt_stream 2): the generation's blocks are dispatched ahead
