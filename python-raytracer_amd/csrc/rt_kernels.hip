@@ -2241,6 +2241,18 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     const int mt_pm = cam->lens_radius != 0.0 ? 15 : 3;  // a pinhole camera reads planes 0 and 1 only
     const srt_ctx::MtBandTab* mt_bt[2] = {nullptr, nullptr};
     int64_t mt_win_need = (int64_t)rtmt::SEGS * rtmt::N;
+    // (the band tables and end polynomials are kept per frame shape; a context that has seen many
+    // shapes drops them between frames, when no frame in flight reads them)
+    if (c->async_pending == 0 && (c->mt_bandtabs.size() >= 16 || c->mt_end_polys.size() >= 64)) {
+        HIP_TRY(hipDeviceSynchronize());
+        for (auto& t : c->mt_bandtabs) {
+            (void)hipFree(t.bands);
+            (void)hipFree(t.polys);
+        }
+        c->mt_bandtabs.clear();
+        for (auto& e : c->mt_end_polys) (void)hipFree(e.second);
+        c->mt_end_polys.clear();
+    }
     if (use_mt && c->mt_bands_on && n_rows < Hf) {
         const int last_ns = a->spp - (F.npass - 1) * batch;
         for (int k = 0; k < 2; ++k) {

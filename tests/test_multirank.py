@@ -377,3 +377,29 @@ def test_gpu_async_band_mode_shard_frames_match_sync_frames(world):
         lib.srt_set_option(ctx, b"rehearse_shard", 0)
         for h in hosts:
             lib.srt_host_free(ctx, h)
+
+
+@pytest.mark.gpu
+def test_gpu_many_shard_shapes_keep_band_mode_exact():
+    """More row sets than the context keeps band tables for (16): the tables are dropped between
+    frames and rebuilt; every shard still equals the tabulated stream's render and numpy's state
+    advances identically."""
+    import scenes
+    from sightpy import _backend as B
+    from sightpy._shard import shard_rows
+
+    W, H = 64, 80
+    sc = scenes.example1(W, H, 3)
+    cases = [(n, r) for n in (2, 3, 4, 5, 6, 7) for r in range(3) if r < n][:18]
+    try:
+        for n, r in cases:
+            rows = shard_rows(H, n, r)
+            out = {}
+            for bands in (1, 0):
+                _set_option("mt_bands", bands)
+                np.random.seed(n * 10 + r)
+                out[bands] = (B.render_scene(sc, 2, seed=5, mt=True, rows=rows), np.random.get_state()[1].copy())
+            assert np.array_equal(out[0][0].rgb, out[1][0].rgb), (n, r)
+            assert np.array_equal(out[0][1], out[1][1])
+    finally:
+        _set_option("mt_bands", 1)
