@@ -92,57 +92,83 @@ def _pool_warm(args):
     return os.getpid()
 
 
+def _oracle_samples(sc, jit, rows, counts):
+    """The oracle's get_raycolor of the samples `jit` (rows: a row tile; jit holds its pixels):
+    summed colour.  Monte-Carlo draws come from numpy's global RNG, as in the reference."""
+    import sightpy_oracle as O
+
+    acc = 0.0
+    for j in jit:
+        Oo, Do = O.primary_rays(sc.camera, j, rows)
+        acc = acc + O.raycolor(sc, O.Rays(np.ascontiguousarray(np.broadcast_to(Oo, Do.shape)), Do,
+                                          O.scene_medium(sc), 0), counts)
+    return acc
+
+
 def _pool_task(args):
     """One Pool task: the oracle's get_raycolor of a batch of samples (reference scene.py:16-17,
     98-116: each task traces its samples and returns their summed colour)."""
-    builder, W, H, depth, jit = args
+    builder, W, H, depth, jit, rows = args
     import scenes
-    import sightpy_oracle as O
 
     sc = getattr(scenes, builder)(W, H, depth)
     counts = {}
-    acc = 0.0
-    for j in jit:
-        Oo, Do = O.primary_rays(sc.camera, j)
-        acc = acc + O.raycolor(sc, O.Rays(np.ascontiguousarray(np.broadcast_to(Oo, Do.shape)), Do,
-                                          O.scene_medium(sc), 0), counts)
+    acc = _oracle_samples(sc, jit, rows, counts)
     return acc, sum(counts["depth"].values())
 
 
-def cpu_baseline(builder, W, H, depth, spp, budget_s=15.0):
+# CPU sample per config (BASELINE.md step 4): the headline frames whole; the 4K and 512-spp frames on
+# one row tile (rank 0's rows of an 8-rank job), rates extrapolated to the frame
+CPU_TILE = {"example4_4k_d6": 8, "cornell_800_s512": 8, "mesh_1080p_d3": 8}
+
+
+def cpu_baseline(builder, W, H, depth, spp, frame_rays, tile_of=0, budget_s=15.0):
     """The oracle (numpy restatement of the reference, oracle/sightpy_oracle.py) timed on this host's
-    CPU on the same frame: (1) one core, samples one after another until the frame is done or
-    `budget_s` is spent; (2) a multiprocessing.Pool over samples structured like the reference's
-    Scene.render (scene.py:80-116: ceil(spp / workers) samples per task, results summed), with as
-    many workers as this process may use (capped at 16, the GPU box's CPU share per GPU)."""
+    CPU on the same frame, or on a row tile of it (`tile_of` > 1: rank 0's rows of a tile_of-rank
+    job) for frames whose single sample would run for minutes: (1) one core, samples one after another
+    until the frame (tile) is done or `budget_s` is spent; (2) a multiprocessing.Pool over samples
+    structured like the reference's Scene.render (scene.py:80-116: ceil(spp / workers) samples per
+    task, results summed), with as many workers as this process may use (capped at 16, the GPU box's
+    CPU share per GPU) -- on a tile, min(spp, workers) samples.  The extrapolated frame time is the
+    GPU-counted frame's rays at the measured rate."""
     import multiprocessing as mp
     import scenes
-    import sightpy_oracle as O
+    from sightpy._shard import shard_rows
 
     sc = getattr(scenes, builder)(W, H, depth)
     np.random.seed(0)
-    jit = sc.camera.draw_jitter(spp)
-    counts = {}
-    done = 0
-    t0 = time.perf_counter()
-    for s in range(spp):
-        Oo, Do = O.primary_rays(sc.camera, jit[s])
-        O.raycolor(sc, O.Rays(np.ascontiguousarray(np.broadcast_to(Oo, Do.shape)), Do, O.scene_medium(sc), 0), counts)
-        done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    rays1 = sum(counts["depth"].values())
-    one = {"value": round(rays1 / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-           "sample": "oracle/sightpy_oracle.py, 1 process, OPENBLAS_NUM_THREADS=1: %d of %d samples of the same "
-                     "%dx%d frame (%d rays, %.1f s)" % (done, spp, W, H, rays1, dt)}
+    rows = shard_rows(H, tile_of, 0) if tile_of > 1 else None
+    npx = (len(rows) if rows is not None else H) * W
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
     workers = max(1, min(avail, 16))
-    per_task = -(-spp // workers)
-    tasks = [(builder, W, H, depth, jit[i:i + per_task]) for i in range(0, spp, per_task)]
+    ns = spp if rows is None else min(spp, workers)
+    jit = sc.camera.draw_jitter(ns)
+    if rows is not None:
+        jit = np.ascontiguousarray(jit.reshape(ns, 4, H, W)[:, :, rows].reshape(ns, 4, -1))
+    what = ("the whole %dx%d frame" % (W, H) if rows is None else
+            "a row tile of the %dx%d frame (rank 0's %d rows of an %d-rank job, %d pixels)" % (W, H, len(rows),
+                                                                                             tile_of, npx))
+    counts = {}
+    done = 0
+    t0 = time.perf_counter()
+    for s in range(ns):
+        _oracle_samples(sc, jit[s:s + 1], rows, counts)
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    rays1 = sum(counts["depth"].values())
+    rate1 = rays1 / dt
+    one = {"value": round(rate1 / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
+           "sample": "oracle/sightpy_oracle.py, 1 process, OPENBLAS_NUM_THREADS=1: %d of %d samples of %s "
+                     "(%d rays, %.1f s)" % (done, spp, what, rays1, dt),
+           "frame_s_extrapolated": round(frame_rays / rate1, 2) if rows is not None or done < spp else None,
+           "extrapolated": rows is not None or done < spp}
+    per_task = -(-ns // workers)
+    tasks = [(builder, W, H, depth, jit[i:i + per_task], rows) for i in range(0, ns, per_task)]
     # spawned workers (fresh interpreters: this process holds the GPU, forked children would inherit
     # its device handles), warmed up with the imports and scene build before the timed tasks
     ctx = mp.get_context("spawn")
@@ -152,11 +178,16 @@ def cpu_baseline(builder, W, H, depth, spp, budget_s=15.0):
         res = list(pool.imap_unordered(_pool_task, tasks))
         dtp = time.perf_counter() - t0
     raysp = sum(r[1] for r in res)
-    pool_leg = {"value": round(raysp / dtp / 1e6, 4), "unit": "Mrays/s", "cores": min(workers, len(tasks)),
+    ratep = raysp / dtp
+    pool_leg = {"value": round(ratep / 1e6, 4), "unit": "Mrays/s", "cores": min(workers, len(tasks)),
                 "workers": workers, "kind": "port",
                 "sample": "oracle/sightpy_oracle.py in multiprocessing.Pool(%d) over samples like scene.py:80-116 "
-                          "(%d tasks of %d sample(s)): the whole %dx%d %d-spp frame (%d rays, %.2f s wall incl. "
-                          "the scene build per task)" % (workers, len(tasks), per_task, W, H, spp, raysp, dtp)}
+                          "(%d tasks of %d sample(s)): %d of %d samples of %s (%d rays, %.2f s wall incl. the scene "
+                          "build per task)" % (workers, len(tasks), per_task, ns, spp, what, raysp, dtp),
+                "frame_s_extrapolated": round(frame_rays / ratep, 2) if rows is not None else round(dtp, 2),
+                "extrapolated": rows is not None,
+                "note": "the reference splits a frame over samples, one task per ceil(spp / cpus) samples, so it "
+                        "keeps at most spp cores busy (%d here) however many the host has" % spp}
     one.update({"cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "usable_cpus": avail, "pool": pool_leg})
     return one
 
@@ -203,12 +234,11 @@ def roofline(kname, kms, model_bytes, frame_path, krec, src):
         roof["ridge_flop_per_byte"] = round(ridge, 2)
         roof["fp64"] = {"achieved_TFLOPs": round(tf, 3), "peak": FP64_PEAK_TFS, "frac": round(tf / FP64_PEAK_TFS, 4),
                         "note": "64 x (ADD + MUL + TRANS + 2 FMA) f64 wave instructions: counts masked lanes"}
-    if "SQ_INSTS_VALU" in c and "SQ_INSTS_VALU_FMA_F64" in c:
-        f64 = c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_FMA_F64"]
-        cycles = 4 * f64 + 2 * (c["SQ_INSTS_VALU"] - f64)  # wave64 on SIMD32: 2 cycles, f64 at half rate: 4
-        roof["valu_issue_frac"] = round(cycles / (1024 * sec * 2.4e9), 4)
-    if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
-        roof["wave_wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+    # (tools/pmc_summary.py: VALU issue cycles over the dispatch's SIMD cycles, GRBM_GUI_ACTIVE / 8 XCDs)
+    if krec.get("valu_issue_frac") is not None:
+        roof["valu_issue_frac"] = round(krec["valu_issue_frac"], 4)
+    if krec.get("wave_wait_frac") is not None:
+        roof["wave_wait_frac"] = round(krec["wave_wait_frac"], 4)
     if "valu_issue_frac" in roof and "wave_wait_frac" in roof:
         roof["limiter"] = ("latency: 2 waves/SIMD (register-bound); waves wait on memory %.0f%% of their cycles, VALU "
                            "issue %.0f%% busy, HBM %.0f%% of peak" % (100 * roof["wave_wait_frac"],
@@ -257,6 +287,61 @@ def comm_id_exchange(lib, N, rank, world):
     return buf, path
 
 
+def visible_gpus():
+    """GPUs this process may use, counted WITHOUT initialising HIP (the launcher below must not touch
+    the GPU before it starts the ranks): KFD topology nodes with SIMDs (GPU agents), capped by the
+    HIP/ROCR/CUDA_VISIBLE_DEVICES lists; rocminfo (a child process) if sysfs is unreadable."""
+    n = None
+    topo = Path("/sys/class/kfd/kfd/topology/nodes")
+    try:
+        n = 0
+        for node in topo.iterdir():
+            props = (node / "properties").read_text().split("\n")
+            simd = [ln.split()[1] for ln in props if ln.startswith("simd_count ")]
+            if simd and int(simd[0]) > 0:
+                n += 1
+    except (OSError, ValueError, IndexError):
+        n = None
+    if n is None:
+        try:
+            out = subprocess.run(["/opt/rocm/bin/rocminfo"], capture_output=True, text=True, timeout=60).stdout
+            n = sum(1 for ln in out.splitlines() if ln.strip().startswith("Name:") and "gfx" in ln)
+        except (OSError, subprocess.SubprocessError):
+            n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def launch_plan(gpus, env, n_visible, argv):
+    """How `bench.py --gpus N` runs: None = in this process (N == WORLD_SIZE, one rank per GPU, as the
+    driver launches it through torch.distributed.run); a command = start N ranks through
+    torch.distributed.run as a child process (WORLD_SIZE unset, N > 1).  Refuses (SystemExit, rc 2)
+    rather than measure fewer GPUs than asked: fewer than N GPUs visible, or a launcher whose
+    WORLD_SIZE differs from N."""
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks" % (gpus, world))
+        return None
+    if gpus == 1:
+        return None
+    if n_visible < gpus:
+        raise SystemExit("bench.py: --gpus %d but only %d GPU(s) visible; refusing to report an N=%d line "
+                         "measured on fewer GPUs" % (gpus, n_visible, gpus))
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + list(argv)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -275,9 +360,21 @@ def main():
                     help="diagnostic: synchronous timed frames (no pipelining), so a rocprofv3 kernel trace shows each "
                          "kernel's launch time alone, as the roofline's HIP-event kernel_ms measures it")
     ap.add_argument("--shard-of", type=int, default=0,
-                    help="diagnostic (1 GPU): render only rank 0's rows of an N-rank job (its per-frame work "
+                    help="diagnostic (1 GPU): render only one rank's rows of an N-rank job (its per-frame work "
                          "without the gather)")
+    ap.add_argument("--shard-rank", default="0",
+                    help="with --shard-of: the rank rehearsed, or 'all' (every rank in turn; ms_per_step = the "
+                         "slowest rank, value = all ranks' rays / that time)")
+    ap.add_argument("--shard-bands", type=int, default=0,
+                    help="most row bands per rank (library option shard_bands; default rt_device.h SHARD_BANDS)")
     args = ap.parse_args()
+
+    cmd = launch_plan(args.gpus, os.environ, visible_gpus() if "WORLD_SIZE" not in os.environ and args.gpus > 1
+                      else args.gpus, sys.argv[1:])
+    if cmd is not None:
+        # one process per GPU: the ranks are children of torch.distributed.run (nothing here has
+        # touched the GPU); rank 0 prints the line
+        sys.exit(subprocess.run(cmd).returncode)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -306,7 +403,14 @@ def main():
         if rank != 0:
             shm_frames = shared_frames(False, world, NOUT, 3 * W * H * 8)
         N.check(lib, lib.srt_comm_init(ctx, world, rank, cid))
+    nr, rk = ctypes.c_int(0), ctypes.c_int(0)
+    N.check(lib, lib.srt_comm_rank(ctx, ctypes.byref(nr), ctypes.byref(rk)))
+    if (nr.value, rk.value) != (world, rank):
+        raise SystemExit("bench.py: the library's communicator has %d ranks (this is %d), the launcher %d (rank %d)"
+                         % (nr.value, rk.value, world, rank))
     N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))  # size every frame slot during the warmup
+    if args.shard_bands:
+        N.check(lib, lib.srt_set_option(ctx, b"shard_bands", args.shard_bands))
     for kv in args.option:
         k, v = kv.split("=")
         N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
@@ -315,11 +419,15 @@ def main():
     npix_full = W * H
     flags = N.RENDER_SHARDED | N.RENDER_RGB_ROWS if world > 1 else 0
     rows32 = None
-    if args.shard_of > 1 and world == 1:
-        from sightpy._shard import shard_rows
+    from sightpy._shard import SHARD_BANDS, band_height, shard_rows
 
-        rows32 = np.ascontiguousarray(shard_rows(H, args.shard_of, 0), dtype=np.int32)
-        npix_full = len(rows32) * W  # the shard's outputs
+    kmax = args.shard_bands or SHARD_BANDS
+    rehearse = {None: None}  # rank -> its rows (None: the frame as the launcher splits it)
+    if args.shard_of > 1 and world == 1:
+        ranks = range(args.shard_of) if args.shard_rank == "all" else [int(args.shard_rank)]
+        rehearse = {r: np.ascontiguousarray(shard_rows(H, args.shard_of, r, kmax), dtype=np.int32) for r in ranks}
+        rows32 = rehearse[min(ranks)]
+        npix_full = max(len(v) for v in rehearse.values()) * W  # the shards' outputs
 
     # outputs: the whole frame in pinned host memory, one pair of buffers per frame in flight (N > 1:
     # the uint8 image on rank 0, gathered over RCCL; the linear RGB in the shared frames, every rank)
@@ -361,18 +469,29 @@ def main():
         if world > 1:
             N.check(lib, lib.srt_comm_barrier(ctx))
 
-    for w in range(args.warmup):
-        step(async_ok=w > 0)  # the first frame runs synchronously (sizes queues and rings)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(async_ok=not args.sync)
-    last = N.Stats()
-    N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(last)))  # every frame in host memory, flags checked
-    if world > 1:
-        N.check(lib, lib.srt_comm_barrier(ctx))
-    elapsed = time.perf_counter() - t0
-    last = last.as_dict()
+    rank_ms, rank_rays, enq = [], [], []
+    for rr, rows_r in rehearse.items():
+        if rows_r is not None:
+            rows32 = rows_r
+            a.rows, a.n_rows = N.ptr(rows32), len(rows32)
+        for w in range(args.warmup):
+            step(async_ok=w > 0)  # the first frame runs synchronously (sizes queues and rings)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(async_ok=not args.sync)
+        enq.append((time.perf_counter() - t0) / args.steps * 1e3)  # host time to queue a frame
+        last = N.Stats()
+        N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(last)))  # every frame in host memory, flags checked
+        if world > 1:
+            N.check(lib, lib.srt_comm_barrier(ctx))
+        el = time.perf_counter() - t0
+        last = last.as_dict()
+        rank_ms.append(el / args.steps * 1e3)
+        rank_rays.append(last["total_rays"])
+    elapsed = max(rank_ms) * args.steps / 1e3
+    if len(rehearse) > 1:
+        last["total_rays"] = sum(rank_rays)
     vals = (ctypes.c_double * 2)(elapsed, float(last["total_rays"]))
     if world > 1:
         N.check(lib, lib.srt_comm_allreduce(ctx, vals, 1, 1))  # max elapsed over ranks
@@ -435,6 +554,7 @@ def main():
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
+            "nranks": nr.value,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
@@ -451,12 +571,20 @@ def main():
                        "parallelism": "row-band shards x%d: uint8 tiles gathered to rank 0 over RCCL (xGMI); every rank "
                                       "writes its rows of the linear RGB into the shared host frame over its own "
                                       "PCIe link" % world
-                       if world > 1 else ("diagnostic: rank 0's rows of a %d-rank job, no gather" % args.shard_of
-                                          if rows32 is not None else "1 GPU"),
+                       if world > 1 else (("diagnostic: rank %s's rows of a %d-rank job, no gather" % (
+                                              args.shard_rank, args.shard_of) if len(rehearse) == 1 else
+                                              "diagnostic: every rank's rows of a %d-rank job rendered in turn on "
+                                              "one GPU, no gather; ms_per_step = the slowest rank's frame"
+                                              % args.shard_of) if rows32 is not None else "1 GPU"),
                        "frame": "render() entry (scene resident) -> jitter stream on the GPU -> all samples and depths "
                                 "-> sRGB resolve -> uint8 + linear RGB (f64) in pinned host memory; frames pipelined",
-                       "frame_ms": round(ms_step, 4)},
+                       "frame_ms": round(ms_step, 4),
+                       "host_enqueue_ms": round(max(enq), 4),
+                       "row_bands": {"kmax": kmax, "band_height": band_height(H, max(world, args.shard_of, 1), kmax)}},
         }
+        if len(rehearse) > 1:
+            rec["rank_frame_ms"] = [round(x, 4) for x in rank_ms]
+            rec["rank_rays"] = rank_rays
         if sec:
             rec["config"]["frame_latency_ms"] = sec["frame_latency_ms"]
             if "device_resident" in sec:
@@ -482,7 +610,7 @@ def main():
                                       "frame's tail with the next, so ms_per_step can be below it")
             rec["roofline"] = roof
         if not args.no_cpu_baseline and world == 1:
-            rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth, spp)
+            rec["cpu_baseline"] = cpu_baseline(builder, W, H, depth, spp, total_rays, CPU_TILE.get(args.config, 0))
         print(json.dumps(rec), flush=True)
     if world > 1:
         N.check(lib, lib.srt_comm_barrier(ctx))

@@ -568,11 +568,14 @@ def hit_ids(scene, O, D):
 
 
 # ---- camera and render driver (camera.py:51-85, scene.py:71-140) -----------------------------
-def primary_rays(cam, j):
-    """j: (4, n) uniforms [x-jitter, y-jitter, disk r, disk phi] -> O, D (3, n)."""
+def primary_rays(cam, j, rows=None):
+    """j: (4, n) uniforms [x-jitter, y-jitter, disk r, disk phi] -> O, D (3, n).  `rows`: only these
+    image rows (a row shard of a multi-GPU frame; j holds their pixels, row-major)."""
     W, H = cam.screen_width, cam.screen_height
     xs = np.linspace(-cam.camera_width / 2.0, cam.camera_width / 2.0, W)
     ys = np.linspace(cam.camera_height / 2.0, -cam.camera_height / 2.0, H)
+    if rows is not None:
+        ys = ys[np.asarray(rows)]
     xx, yy = np.meshgrid(xs, ys)
     x = xx.flatten() + (j[0] - 0.5) * cam.camera_width / W
     y = yy.flatten() + (j[1] - 0.5) * cam.camera_height / H
@@ -589,10 +592,12 @@ def scene_medium(scene):
     return np.array([[scene.n.x], [scene.n.y], [scene.n.z]])
 
 
-def render_linear(scene, jitter, stream=None, sample_base=0):
+def render_linear(scene, jitter, stream=None, sample_base=0, rows=None):
     """Sum over samples of raycolor / spp.  jitter (spp, 4, n).  Returns rgb (3, n), hit ids
     (spp, n) of the primary rays and the per-depth / shadow ray counts.  `stream`: a DeviceStream
-    for the Monte-Carlo draws (default: numpy's global RNG, the reference's order)."""
+    for the Monte-Carlo draws (default: numpy's global RNG, the reference's order).  `rows`: render
+    only these image rows (a row shard; jitter holds their pixels), the Monte-Carlo draws keyed by
+    global pixel as on the device."""
     spp = jitter.shape[0]
     counts = {}
     acc = 0.0
@@ -600,12 +605,15 @@ def render_linear(scene, jitter, stream=None, sample_base=0):
     _RNG["stream"] = stream
     try:
         for s in range(spp):
-            O, D = primary_rays(scene.camera, jitter[s])
+            O, D = primary_rays(scene.camera, jitter[s], rows)
             ids.append(hit_ids(scene, O, D)[1])
             r = Rays(O, D, scene_medium(scene), 0, 0)
             if stream is not None:
                 n = D.shape[1]
-                r.pix = np.arange(n, dtype=np.uint32)
+                W = int(scene.camera.screen_width)
+                r.pix = (np.arange(n, dtype=np.uint32) if rows is None else
+                         (np.asarray(rows, dtype=np.uint32)[:, None] * np.uint32(W) +
+                          np.arange(W, dtype=np.uint32)[None, :]).reshape(-1))
                 r.path = np.full(n, mix32(PRIMARY_PATH, sample_base + s), dtype=np.uint32)
             acc = acc + raycolor(scene, r, counts)
     finally:

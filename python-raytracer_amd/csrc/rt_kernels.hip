@@ -161,6 +161,21 @@ constexpr double FX_SCALE = (double)(1ull << FX_BITS);
 constexpr double FX_UNIT = 1.0 / FX_SCALE;
 constexpr double FX_MAX = 131072.0;                 // 2^17
 
+// Range of the sums: a pixel-channel sum wraps only beyond 2^20 (2^64 scaled).  Besides the three
+// sums, every pixel keeps a coarse magnitude -- the f32 sum of |r| + |g| + |b| of its terms, one
+// more fire-and-forget atomic (fx_mag, behind the sums in the same buffer) -- and the resolve
+// distrusts a pixel whose magnitude reached FX_MAG_LIMIT (2^16; f32 rounding keeps it within a factor
+// 1 + n 2^-24 of the true magnitude, so no sum of fewer than 2^23 terms gets near 2^20 unseen).
+// A returning atomic per term (checking each partial sum) cost 6.6 % of the device frame.
+constexpr float FX_MAG_LIMIT = 65536.0f;
+RT_HD int64_t fx_words(int64_t npix) { return 3 * npix + (npix + 1) / 2; }  // u64 words of fbx
+__device__ __forceinline__ float* fx_mag(unsigned long long* fbx, int64_t npix) {
+    return reinterpret_cast<float*>(fbx + 3 * npix);
+}
+__device__ __forceinline__ const float* fx_mag(const unsigned long long* fbx, int64_t npix) {
+    return reinterpret_cast<const float*>(fbx + 3 * npix);
+}
+
 __device__ __forceinline__ bool fx_add(unsigned long long* acc, double v) {
     if (!(fabs(v) < FX_MAX)) return false;  // (also NaN)
     atomicAdd(acc, (unsigned long long)__double2ll_rn(v * FX_SCALE));
@@ -176,9 +191,10 @@ __device__ __forceinline__ void fb_add(double* fb, unsigned long long* fbx, uint
 #endif
     if (fbx) {
         // all three channels added (no short-circuit), then one range check
-        const int ok = (int)fx_add(fbx + pix, w.x * c.x) & (int)fx_add(fbx + npix + pix, w.y * c.y) &
-                       (int)fx_add(fbx + 2 * npix + pix, w.z * c.z);
+        const double tx = w.x * c.x, ty = w.y * c.y, tz = w.z * c.z;
+        const int ok = (int)fx_add(fbx + pix, tx) & (int)fx_add(fbx + npix + pix, ty) & (int)fx_add(fbx + 2 * npix + pix, tz);
         if (!ok) atomicOr(flags + 1, RETRY_FIXED_RANGE);
+        unsafeAtomicAdd(fx_mag(fbx, npix) + pix, (float)((fabs(tx) + fabs(ty)) + fabs(tz)));
     } else {
         unsafeAtomicAdd(fb + pix, w.x * c.x);
         unsafeAtomicAdd(fb + npix + pix, w.y * c.y);
@@ -190,15 +206,11 @@ __device__ __forceinline__ double fx_value(const unsigned long long* fbx, int64_
     return (double)(long long)fbx[ch * npix + p] * FX_UNIT;
 }
 
-// a pixel-channel sum the resolve must not trust: negative (no material of the reference adds a
-// negative term, so a wrapped sum of non-negative terms) or >= 2^18 (half the range: the sum grew
-// towards the wrap).  A sum that wrapped twice (a pixel-channel total >= 2^20) is not detectable.
+// a pixel the resolve must not trust: its coarse magnitude reached FX_MAG_LIMIT (or is NaN), or a
+// channel sum lies in [2^61, 2^64) scaled (>= 2^17 in colour units; negative = wrapped)
 __device__ __forceinline__ bool fx_suspect(const unsigned long long* fbx, int64_t npix, int64_t p) {
-    bool bad = false;
-    for (int ch = 0; ch < 3; ++ch) {
-        const long long v = (long long)fbx[ch * npix + p];
-        bad |= (v < 0) | (v >= (1ll << 62));
-    }
+    bool bad = !(fx_mag(fbx, npix)[p] < FX_MAG_LIMIT);
+    for (int ch = 0; ch < 3; ++ch) bad |= (fbx[ch * npix + p] >> 61) != 0;
     return bad;
 }
 
@@ -469,6 +481,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             if (P.fbx) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = 0ull;  // this frame's fixed-point sums start here
+                fx_mag(P.fbx, P.npix)[p] = 0.0f;
             }
         } else if (active && !is_zero(acc)) {
             P.fb[p] += acc.x;
@@ -1036,7 +1049,6 @@ __global__ __launch_bounds__(BLOCK) void k_primary_rays(srt_camera cam, const do
 
 // ---- row-band shards (SRT_RENDER_SHARDED, rt_device.h shard_of_row) -----------------------------
 // Rank 0 gathers every rank's tiles (RCCL) and k_assemble writes them into the frame.
-constexpr int BAND = SHARD_BAND;
 constexpr int MAX_RANKS = 64;
 struct GatherTiles {
     const uint8_t* u8[MAX_RANKS];  // [rows_q][W][3]
@@ -1044,13 +1056,13 @@ struct GatherTiles {
     int64_t npix[MAX_RANKS];       // rows_q * W
 };
 
-__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t W, int64_t H, uint8_t* u8,
-                                                   double* rgb) {
+__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t band, int64_t W, int64_t H,
+                                                   uint8_t* u8, double* rgb) {
     const int64_t n = W * H;
     for (int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x; g < n; g += (int64_t)gridDim.x * BLOCK) {
         const int64_t y = g / W, x = g - y * W;
-        const int q = shard_of_row(y, nranks);
-        const int64_t l = shard_local_row(y, nranks) * W + x;
+        const int q = shard_of_row(y, nranks, band);
+        const int64_t l = shard_local_row(y, nranks, band) * W + x;
         if (u8) {
             const uint8_t* s = T.u8[q] + 3 * l;
             u8[3 * g] = s[0]; u8[3 * g + 1] = s[1]; u8[3 * g + 2] = s[2];
@@ -1063,10 +1075,10 @@ __global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, i
     }
 }
 
-std::vector<int32_t> band_rows(int64_t H, int n, int q) {
+std::vector<int32_t> band_rows(int64_t H, int n, int q, int64_t band) {
     std::vector<int32_t> r;
     for (int64_t y = 0; y < H; ++y)
-        if (shard_of_row(y, n) == q) r.push_back((int32_t)y);
+        if (shard_of_row(y, n, band) == q) r.push_back((int32_t)y);
     return r;
 }
 
@@ -1140,7 +1152,7 @@ struct FrameSlot {
     // frame buffers
     double* fb = nullptr;
     int64_t fb_cap = 0;
-    unsigned long long* fbx = nullptr;  // [3][npix] fixed-point sums (fb_add)
+    unsigned long long* fbx = nullptr;  // [3][npix] fixed-point sums + [npix] f32 magnitudes (fb_add)
     int64_t fbx_cap = 0;
     double* rgb = nullptr;
     int64_t rgb_cap = 0;
@@ -1168,7 +1180,7 @@ struct FrameSlot {
     // the frame's gather (srt_render_group posts it for all its contexts in one RCCL group)
     struct Gather {
         bool on = false;
-        int64_t W = 0, H = 0, npix = 0, maxpix = 0;
+        int64_t W = 0, H = 0, npix = 0, maxpix = 0, band = 1;
         bool want_u8 = false, want_rgb = false;
         uint8_t* dst_u8 = nullptr;  // where k_assemble writes (caller's device buffer or full_u8)
         double* dst_rgb = nullptr;
@@ -1278,6 +1290,8 @@ struct srt_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     bool defer_gather = false;  // srt_render_group posts the gathers of all its contexts in one group
+    bool retry_frame = false;   // the last finish_async failed only with RETRY_* bits (render the frame again)
+    int shard_bands = SHARD_BANDS;  // option "shard_bands": most row bands per rank (rt_device.h shard_band_height)
     double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
@@ -1795,6 +1809,7 @@ void free_slot(FrameSlot& f) {
 // stats of the last).  An overflow grows the queues and is reported as an error: those frames are
 // wrong and must be rendered again.  Leaves slot 0 current.
 int finish_async(srt_ctx* c, srt_stats* st) {
+    c->retry_frame = false;
     if (c->async_pending == 0) {
         c->f = &c->slots[0];
         if (st) *st = c->async_stats;
@@ -1838,6 +1853,7 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     }
     c->f = &c->slots[0];
     if (first_err) return first_err;
+    c->retry_frame = overflow;
     if (overflow)
         return fail(SRT_ERR_MEMORY, "a ray queue overflowed (queues grown), a tie met chain mode (chain mode "
                                     "off) or a colour left the fixed-point range (f64 sums from now on) during an "
@@ -1847,9 +1863,7 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     return SRT_OK;
 }
 
-int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) {
-    return (int64_t)band_rows(G.H, nranks, q).size() * G.W;
-}
+int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) { return shard_rank_rows(G.H, nranks, q, G.band) * G.W; }
 
 // Post this rank's part of the frame's gather on its stream (inside an RCCL group): rank 0 receives
 // every other rank's uint8 (and linear-RGB) tile, the others send theirs.
@@ -1895,7 +1909,7 @@ int gather_finish(srt_ctx* c) {
         T.npix[q] = shard_npix(G, c->nranks, q);
     }
     hipStream_t st = c->f->stream;
-    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.W, G.H,
+    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.band, G.W, G.H,
                        G.want_u8 ? G.dst_u8 : nullptr, G.want_rgb ? G.dst_rgb : nullptr);
     HIP_TRY(hipGetLastError());
     if (G.host_u8) HIP_TRY(hipMemcpyAsync(G.host_u8, G.dst_u8, (size_t)3 * G.W * G.H, hipMemcpyDeviceToHost, st));
@@ -1971,6 +1985,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "shard_bands")) {
+        if (value < 1 || value > 4096) return fail(SRT_ERR_ARG, "shard_bands: 1..4096");
+        c->shard_bands = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
@@ -2162,12 +2181,13 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     std::vector<int32_t> rows_h;
     const int32_t* rows_src = nullptr;
     int n_rows = a->n_rows;
+    int64_t band = 1;  // row-band height of a sharded frame
     if (sharded) {
         if (c->nranks > MAX_RANKS) return fail(SRT_ERR_ARG, "too many ranks");
-        if (cam->height < (int64_t)BAND * c->nranks)
-            return fail(SRT_ERR_ARG, "a sharded frame needs at least 8 rows per rank");
+        if (cam->height < c->nranks) return fail(SRT_ERR_ARG, "a sharded frame needs at least one row per rank");
         if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
-        rows_h = band_rows(cam->height, c->nranks, c->rank);
+        band = shard_band_height(cam->height, c->nranks, c->shard_bands);
+        rows_h = band_rows(cam->height, c->nranks, c->rank, band);
         n_rows = (int)rows_h.size();
         rows_src = rows_h.data();
     } else if (a->rows) {
@@ -2262,13 +2282,13 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!mt_bt[0] || !mt_bt[1]) mt_bt[0] = mt_bt[1] = nullptr;
     }
     const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * W * Hf : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
-    const int64_t maxpix = sharded ? (int64_t)band_rows(Hf, c->nranks, 0).size() * W : 0;  // rank 0 has the most rows
+    const int64_t maxpix = sharded ? shard_rank_rows(Hf, c->nranks, 0, band) * W : 0;  // rank 0 has the most rows
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
     // for them (and reports their errors)
     if (async && c->async_pending > 0) {
         const FramePlan& pp = c->f->pending ? c->f->plan : c->slots[c->last_slot].plan;
         const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && n_rows <= c->cam_cap[2] &&
-                          3 * npix <= c->f->fb_cap && 3 * npix <= c->f->fbx_cap && 3 * npix <= c->f->rgb_cap &&
+                          3 * npix <= c->f->fb_cap && fx_words(npix) <= c->f->fbx_cap && 3 * npix <= c->f->rgb_cap &&
                           3 * npix <= c->f->u8_cap &&
                           jit_doubles <= c->f->jit_cap && (!use_mt || mt_win_need <= c->f->mt_win_cap) &&
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
@@ -2306,7 +2326,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         c->f = &fs;
         int r = SRT_OK;
         if (!r) r = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * npix);
-        if (!r) r = ensure_buf(&c->f->fbx, c->f->fbx_cap, 3 * npix);
+        if (!r) r = ensure_buf(&c->f->fbx, c->f->fbx_cap, fx_words(npix));
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
@@ -2430,7 +2450,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 if (P.spt < ns && p == 0) {
                     HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * npix * 8, c->f->stream));
                     if (c->deterministic && c->fx_ok)
-                        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)3 * npix * 8, c->f->stream));
+                        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)fx_words(npix) * 8, c->f->stream));
                 }
             }
             P.npix = npix;
@@ -2567,11 +2587,11 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
         c->f->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
-        // this rank's rows of the linear RGB into the shared host frame: per plane, the full 8-row
-        // bands as one pitched copy (the rank's band b is frame rows 8 (b nranks + rank) ..), then a
-        // short last band
+        // this rank's rows of the linear RGB into the shared host frame: per plane, the full bands as
+        // one pitched copy (the rank's band b is frame rows band (b nranks + rank) ..), then a short
+        // last band
         if (rgb_rows) {
-            const int64_t band_px = (int64_t)BAND * W;
+            const int64_t band_px = band * W;
             const int64_t nb = npix / band_px, tail = npix - nb * band_px;
             for (int pl = 0; pl < 3; ++pl) {
                 double* dst = a->out_rgb + (int64_t)pl * W * Hf;
@@ -2594,6 +2614,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             G.H = Hf;
             G.npix = npix;
             G.maxpix = maxpix;
+            G.band = band;
             G.want_u8 = true;
             G.want_rgb = gather_rgb;
             if (c->rank == 0) {
@@ -2722,7 +2743,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
         HIP_TRY(hipMemcpyAsync(dfo, fo, (size_t)n * 8, hipMemcpyDefault, c->f->stream));
     }
     if ((rc = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * n))) return rc;
-    if ((rc = ensure_buf(&c->f->fbx, c->f->fbx_cap, 3 * n))) return rc;
+    if ((rc = ensure_buf(&c->f->fbx, c->f->fbx_cap, fx_words(n)))) return rc;
     if ((rc = ensure_queues(c, n * c->fanout))) return rc;
     // depths a->depth .. a->depth + cap (the batch's depth is a scalar in the reference)
     const int d0 = a->depth;
@@ -2733,7 +2754,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
     for (int attempt = 0;; ++attempt) {
         if (attempt > 8) { rc = fail(SRT_ERR_MEMORY, "ray queues keep overflowing"); break; }
         HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * n * 8, c->f->stream));
-        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)3 * n * 8, c->f->stream));
+        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)fx_words(n) * 8, c->f->stream));
         HIP_TRY(hipMemsetAsync(c->f->counts, 0, (size_t)SRT_MAX_DEPTHS * NSHARD * 4, c->f->stream));
         HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
         HIP_TRY(hipMemsetAsync(c->f->shadow, 0, 8 * NSHARD, c->f->stream));
@@ -3082,6 +3103,10 @@ int srt_comm_rank(srt_ctx* c, int* nranks, int* rank) {
     return SRT_OK;
 }
 
+}  // extern "C"
+static int render_group_once(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a, srt_stats* st);
+extern "C" {
+
 int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
     if (!ctxs || n < 1 || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
     for (int q = 0; q < n; ++q)
@@ -3089,6 +3114,25 @@ int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_ren
             return fail(SRT_ERR_ARG, "contexts must be the ranks 0..n-1 of one srt_comm_init_all group");
     if (a->jitter) return fail(SRT_ERR_ARG, "a group frame draws its jitter on the devices (mt or Philox)");
     if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
+    // A frame whose passes overflowed a queue/ring, met a chain-mode tie or left the fixed-point range
+    // is rendered again on every context (the gather pairs the ranks' tiles), from the same numpy
+    // state, as the synchronous single-GPU path does; the contexts already grew their queues or
+    // dropped chain mode / fixed-point sums in finish_async.
+    srt_mt_state mt0{};
+    if (a->mt) mt0 = *a->mt;
+    int rc = SRT_OK;
+    for (int attempt = 0;; ++attempt) {
+        if (a->mt) *a->mt = mt0;
+        rc = render_group_once(ctxs, n, cam, a, st);
+        bool again = false;
+        for (int q = 0; q < n; ++q) again |= ctxs[q]->retry_frame;
+        if (rc == SRT_OK || !again || attempt >= 8) return rc;
+    }
+}
+
+}  // extern "C"
+
+static int render_group_once(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
     const bool want_rgb = a->out_rgb != nullptr;
     int rc = SRT_OK;
     srt_render_args aq = *a;
@@ -3137,6 +3181,8 @@ int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_ren
     if (st) *st = sum;
     return SRT_OK;
 }
+
+extern "C" {
 
 int srt_comm_allreduce(srt_ctx* c, double* vals, int n, int op) {
     if (!c || !vals || n < 1 || n > 64 || op < 0 || op > 1) return fail(SRT_ERR_ARG, "bad allreduce arguments");

@@ -30,8 +30,26 @@ def library():
     return _STATE["lib"]
 
 
+def _env_options(lib, ctx):
+    """Options every context of this process takes from the environment (the process context and
+    the contexts of a multi-GPU group alike)."""
+    if os.environ.get("SIGHTPY_FRAME_KERNEL") is not None:  # A/B switch: 0 = per-depth wavefront kernels
+        N.check(lib, lib.srt_set_option(ctx, b"frame_kernel", int(os.environ["SIGHTPY_FRAME_KERNEL"])))
+    if os.environ.get("SIGHTPY_DETERMINISTIC") is not None:  # 0: f64 atomics instead of fixed-point sums
+        N.check(lib, lib.srt_set_option(ctx, b"deterministic", int(os.environ["SIGHTPY_DETERMINISTIC"])))
+
+
+def _device_spec():
+    """$SIGHTPY_DEVICES as a list of ints, or None (unset / empty / "all")."""
+    spec = os.environ.get("SIGHTPY_DEVICES", "").strip()
+    if not spec or spec == "all":
+        return None
+    return [int(v) for v in spec.split(",") if v.strip()]
+
+
 def context():
-    """The process's device context (device = $SIGHTPY_DEVICE, else $LOCAL_RANK, else 0)."""
+    """The process's device context: device = $SIGHTPY_DEVICE, else a one-entry $SIGHTPY_DEVICES,
+    else $LOCAL_RANK, else 0."""
     if _STATE["ctx"] is None:
         lib = library()
         n = ctypes.c_int(0)
@@ -41,11 +59,18 @@ def context():
                 "no HIP device visible (%s); sightpy on MI355X has no CPU fallback"
                 % lib.srt_last_error().decode(errors="replace")
             )
-        dev = int(os.environ.get("SIGHTPY_DEVICE", os.environ.get("LOCAL_RANK", "0"))) % n.value
+        spec = _device_spec()
+        if os.environ.get("SIGHTPY_DEVICE") is not None:
+            dev = int(os.environ["SIGHTPY_DEVICE"])
+        elif spec is not None and len(spec) == 1:
+            dev = spec[0]
+        else:
+            dev = int(os.environ.get("LOCAL_RANK", "0"))
+        if not 0 <= dev < n.value:
+            raise ValueError("sightpy: device %d requested, %d visible" % (dev, n.value))
         ctx = ctypes.c_void_p()
         N.check(lib, lib.srt_create(dev, ctypes.byref(ctx)))
-        if os.environ.get("SIGHTPY_FRAME_KERNEL") is not None:  # A/B switch: 0 = per-depth wavefront kernels
-            N.check(lib, lib.srt_set_option(ctx, b"frame_kernel", int(os.environ["SIGHTPY_FRAME_KERNEL"])))
+        _env_options(lib, ctx)
         _STATE["ctx"] = ctx
         _STATE["device"] = dev
     return _STATE["lib"], _STATE["ctx"]
@@ -61,7 +86,7 @@ def devices():
         n = ctypes.c_int(0)
         N.check(library(), library().srt_device_count(ctypes.byref(n)))
         return list(range(n.value))
-    return [int(v) for v in spec.split(",") if v.strip()]
+    return _device_spec()
 
 
 def group():
@@ -75,6 +100,8 @@ def group():
     arr = (ctypes.c_int * len(devs))(*devs)
     ctxs = (ctypes.c_void_p * len(devs))()
     N.check(lib, lib.srt_comm_init_all(len(devs), arr, ctxs))
+    for q in range(len(devs)):
+        _env_options(lib, ctypes.c_void_p(ctxs[q]))
     _STATE["group"] = (devs, ctxs)
     return lib, ctxs
 

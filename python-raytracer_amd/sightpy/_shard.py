@@ -1,35 +1,66 @@
 """Row-band sharding of a frame across GPUs: the partition the library uses (SRT_RENDER_SHARDED,
-csrc/rt_device.h shard_of_row / shard_local_row), restated with numpy for callers and tests.
+csrc/rt_device.h shard_band_height / shard_of_row / shard_local_row), restated with numpy for
+callers and tests.
 
 The reference parallelises `Scene.render` over samples with `multiprocessing.Pool`
-(`sightpy/scene.py:80-116`).  Pixels are independent, so here the frame is split instead: rank r
-owns the rows `{y : (y // band) % world == r}` (bands dealt round-robin, which balances the cheap
-sky rows against the reflective floor rows) and renders them with the same per-pixel random numbers
-the single-GPU render would use; the library gathers the uint8 (and linear-RGB) tiles to rank 0
-over RCCL and assembles the frame there.  The image is independent of the number of ranks.
+(`sightpy/scene.py:80-116`).  Pixels are independent, so here the frame is split instead: the rows
+are cut into bands of h rows (the last one shorter) dealt round-robin, rank r owning the rows
+`{y : (y // h) % world == r}` -- interleaving balances the cheap sky rows against the reflective
+floor rows -- and rendering them with the same per-pixel random numbers the single-GPU render
+would use; the library gathers the uint8 (and linear-RGB) tiles to rank 0 over RCCL and assembles
+the frame there.  The image is independent of the number of ranks.
+
+Every band of a rank is a run of numpy's stream that the rank's generator jumps to (one ~110 us jump
+per band, plane and sample), so h is as large as the balance allows: at most `kmax` bands per rank
+(at least kmax // 2), the fewest rows on the busiest rank first, then the most bands.
 """
 import numpy as np
 
-BAND = 8
+SHARD_BANDS = 8  # kmax (library option "shard_bands")
 
 
-def shard_rows(height, world, rank, band=BAND):
+def rank_rows(height, world, rank, band):
+    """Rows of `rank` with bands of `band` rows (rt_device.h shard_rank_rows)."""
+    B = -(-int(height) // band)
+    if rank >= B:
+        return 0
+    nb = (B - 1 - rank) // world + 1
+    return nb * band - ((B * band - height) if (B - 1) % world == rank else 0)
+
+
+def band_height(height, world, kmax=SHARD_BANDS):
+    """Band height of a `world`-rank frame of `height` rows (rt_device.h shard_band_height)."""
+    height = int(height)
+    if world <= 1 or height <= 1:
+        return max(height, 1)
+    kmax = max(int(kmax), 1)
+    best_h, best_rows = 1, None
+    for k in range(kmax, max(kmax // 2, 1) - 1, -1):
+        h = max(-(-height // (world * k)), 1)
+        m = max(rank_rows(height, world, q, h) for q in range(world))
+        if best_rows is None or m < best_rows:
+            best_h, best_rows = h, m
+    return best_h
+
+
+def shard_rows(height, world, rank, kmax=SHARD_BANDS):
     """Image rows owned by `rank` (ascending)."""
+    h = band_height(height, world, kmax)
     rows = np.arange(int(height))
-    return rows[(rows // band) % world == rank]
+    return rows[(rows // h) % world == rank]
 
 
-def max_shard_rows(height, world, band=BAND):
+def max_shard_rows(height, world, kmax=SHARD_BANDS):
     """Largest per-rank row count (rank 0's: the padded tile height of the gather)."""
-    return max(len(shard_rows(height, world, r, band)) for r in range(world))
+    return max(len(shard_rows(height, world, r, kmax)) for r in range(world))
 
 
-def assemble_index(height, world, band=BAND):
+def assemble_index(height, world, kmax=SHARD_BANDS):
     """For every image row, its position in the gathered buffer of padded tiles:
     `gathered.reshape(world * maxrows, ...)[idx]` is the image."""
-    maxrows = max_shard_rows(height, world, band)
+    maxrows = max_shard_rows(height, world, kmax)
     idx = np.empty(int(height), dtype=np.int64)
     for r in range(world):
-        rows = shard_rows(height, world, r, band)
+        rows = shard_rows(height, world, r, kmax)
         idx[rows] = r * maxrows + np.arange(len(rows))
     return idx

@@ -320,6 +320,52 @@ def test_gpu_colour_beyond_fixed_point_range_falls_back_to_f64_sums():
     np.testing.assert_allclose(out.rgb, rgb_o, rtol=RTOL, atol=ATOL)
 
 
+def test_gpu_fixed_point_sums_near_wrap_fall_back_to_f64_sums():
+    """Every contribution below the per-term limit (2^17), but a pixel's reflected contributions
+    summing past the coarse magnitude limit (rt_kernels.hip FX_MAG_LIMIT, the guard against a
+    fixed-point sum wrapping): the frame is rendered again with f64 atomics and matches the oracle."""
+    from sightpy import Emissive, Sphere, rgb, vec3
+
+    B = _backend()
+    sc = scenes.example1(48, 36, 3)
+    sc.add(Sphere(material=Emissive(color=rgb(3e4, 3e4, 3e4)), center=vec3(0.0, 60.0, -3.0), radius=55.0,
+                  shadow=False, max_ray_depth=3))
+    np.random.seed(6)
+    jit = sc.camera.draw_jitter(2)
+    out = B.render_scene(sc, 2, jitter=jit, seed=1)
+    assert out.stats["retries"] >= 1
+    rgb_o, ids, counts = O.render_linear(sc, jit)
+    np.testing.assert_allclose(out.rgb, rgb_o, rtol=RTOL, atol=ATOL)
+
+
+def test_gpu_group_render_retries_a_frame_on_every_context():
+    """srt_render_group (Scene.render over $SIGHTPY_DEVICES) renders a frame that left the
+    fixed-point range again on every context, as the single-GPU path does, instead of failing."""
+    from sightpy import Emissive, Sphere, rgb, vec3
+
+    B = _backend()
+    sc = scenes.example1(48, 40, 3)
+    sc.add(Sphere(material=Emissive(color=rgb(1e7, 1e7, 1e7)), center=vec3(0.0, 60.0, -3.0), radius=55.0,
+                  shadow=False, max_ray_depth=3))
+    np.random.seed(9)
+    ref = B.render_scene(sc, 2, seed=3, mt=True)
+    assert ref.stats["retries"] >= 1
+    np.random.seed(9)
+    import os
+
+    old = os.environ.get("SIGHTPY_DEVICES")
+    os.environ["SIGHTPY_DEVICES"] = str(B.devices()[0])
+    try:
+        got = B.render_group(sc, 2, seed=3, mt=True)
+    finally:
+        if old is None:
+            os.environ.pop("SIGHTPY_DEVICES")
+        else:
+            os.environ["SIGHTPY_DEVICES"] = old
+    np.testing.assert_allclose(got.rgb, ref.rgb, rtol=1e-12, atol=1e-6)
+    assert got.stats["total_rays"] == ref.stats["total_rays"]
+
+
 def test_gpu_async_numpy_stream_frames_match_sync_frames():
     """Pipelined frames drawing numpy's stream on the device (the bench's frame loop): each frame's key
     window comes from the previous frame's end jump (k_mt_jump's last block) while that frame's

@@ -46,31 +46,46 @@ def test_shard_rows_partition():
             for r, p in enumerate(parts):
                 buf[r * max_shard_rows(H, world) + np.arange(len(p))] = p
             assert np.array_equal(buf[idx], np.arange(H))
-    # 1080 rows over 8 ranks: 135 bands of 8 rows dealt round-robin (one rank gets one band less)
-    assert [len(shard_rows(1080, 8, r)) for r in range(8)] == [136] * 7 + [128]
+    # 1080 rows over 8 ranks: 40 bands of 27 rows, 5 per rank, 135 rows each (the busiest rank has no
+    # more rows than 1080 / 8; kmax = 8 allows 4..8 bands per rank, and 5 is the most that balance)
+    from sightpy._shard import band_height
+
+    assert band_height(1080, 8) == 27
+    assert [len(shard_rows(1080, 8, r)) for r in range(8)] == [135] * 8
+    # ex4 4K over 8 ranks: 270 rows each; cornell 800 over 8: 100 rows each in 5 bands of 20
+    assert [len(shard_rows(2160, 8, r)) for r in range(8)] == [270] * 8
+    assert band_height(800, 8) == 20 and [len(shard_rows(800, 8, r)) for r in range(8)] == [100] * 8
+    # one band per rank allowed: contiguous blocks
+    assert band_height(1080, 8, kmax=1) == 135
 
 
-def _kernel_shard_map(H, n):
+def _kernel_shard_map(H, n, kmax=8):
     import hostcheck as HC
 
     owner = np.empty(H, dtype=np.int32)
     local = np.empty(H, dtype=np.int64)
     lib = HC.lib()
-    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-    lib.hc_shard_map(H, n, owner.ctypes.data, local.ctypes.data)
-    return owner, local
+    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.hc_shard_map.restype = ctypes.c_int64
+    h = lib.hc_shard_map(H, n, kmax, owner.ctypes.data, local.ctypes.data)
+    return owner, local, h
 
 
-@pytest.mark.parametrize("H", [8, 37, 300, 1080, 2160])
+@pytest.mark.parametrize("H", [8, 37, 300, 800, 1080, 2160])
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
-def test_kernel_shard_map_matches_partition(H, n):
-    from sightpy._shard import shard_rows
+@pytest.mark.parametrize("kmax", [1, 4, 8, 17])
+def test_kernel_shard_map_matches_partition(H, n, kmax):
+    from sightpy._shard import shard_rows, band_height, rank_rows
 
-    owner, local = _kernel_shard_map(H, n)
+    owner, local, h = _kernel_shard_map(H, n, kmax)
+    assert h == band_height(H, n, kmax)
     for q in range(n):
-        rows = shard_rows(H, n, q)
+        rows = shard_rows(H, n, q, kmax)
+        assert len(rows) == rank_rows(H, n, q, h)
         assert np.array_equal(np.where(owner == q)[0], rows)
         assert np.array_equal(local[rows], np.arange(len(rows)))
+    # rank 0 holds the most rows (the gather pads every tile to its size)
+    assert max(len(shard_rows(H, n, q, kmax)) for q in range(n)) == len(shard_rows(H, n, 0, kmax))
 
 
 def _gather_worker(rank, world, port, H, W):
@@ -102,7 +117,7 @@ def _gather_worker(rank, world, port, H, W):
             g_u8[q, : 3 * npq] = bu.numpy()
             g_rgb[q, : 3 * npq] = br.numpy()
         # k_assemble with the kernels' map
-        owner, local = _kernel_shard_map(H, world)
+        owner, local, _ = _kernel_shard_map(H, world)
         out_u8 = np.empty((H, W, 3), dtype=np.uint8)
         out_rgb = np.empty((3, H, W))
         for y in range(H):

@@ -33,6 +33,10 @@ for step in "$@"; do
             run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     mttests) run mttests 600 python3 -u -m pytest tests/test_multirank.py tests/test_mt.py tests/test_gpu.py -x -v -m gpu -k "band or shard or mt or numpy_stream or async" --timeout 300 --timeout-method thread -rf ;;
     mctests) run mctests 600 python3 -u -m pytest tests/test_gpu_mc.py -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
+    shardtests) run shardtests 600 python3 -u -m pytest tests/test_gpu_shards.py -x -v -s -m gpu --timeout 300 --timeout-method thread -rf ;;
+    ab) run ab 900 bash tools/ab_bench.sh "tools/_build/libsightpy_hip_old.so python-raytracer_amd/sightpy/libsightpy_hip.so" --steps ${STEPS:-50} ${AB_ARGS:-} ;;
+    shardsweep) for n in ${SHARD_NS:-8}; do for k in ${KMAXS:-2 4 8 17 32}; do run "sweep_${CONFIG:-example1_1080p_d5}_n${n}_k$k" 300 python3 bench.py --config ${CONFIG:-example1_1080p_d5} --no-cpu-baseline --no-secondary --steps ${STEPS:-100} --shard-of $n --shard-rank all --shard-bands $k; done; done
+                run "sweep_${CONFIG:-example1_1080p_d5}_whole" 300 python3 bench.py --config ${CONFIG:-example1_1080p_d5} --no-cpu-baseline --no-secondary --steps ${STEPS:-100} ;;
     mt) run mt 300 python3 tools/mt_timing.py ;;
     api) run api 300 python3 tools/api_timing.py --repeats 5 --profile ;;
     api_prof) run api_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/api_prof -o api --output-format csv -- python3 tools/api_timing.py --repeats 5 ;;

@@ -10,10 +10,19 @@ launch (MI355X_MICROARCH.md § HBM and § Execution model):
   fp64_flop     = 64 x (ADD_F64 + MUL_F64 + TRANS_F64 + 2 x FMA_F64)
                   (wave-instruction counts x 64 lanes: an upper bound, lanes masked off by divergence
                   are counted)
-  valu_issue_frac = SQ_ACTIVE_INST_VALU / (SQ_BUSY_CU_CYCLES or GRBM_GUI_ACTIVE x CUs x 4 SIMDs)
-                  when the counters are present (how busy the VALU issue ports are)
+  GRBM_GUI_ACTIVE is summed over the 8 XCDs: the dispatch's active cycles are GRBM_GUI_ACTIVE / 8.
+  SQ_ACTIVE_INST_* and SQ_WAVE_CYCLES / SQ_WAIT_* count quad-cycles (x 4 = cycles).
+  valu_issue_frac = (4 x f64 VALU instructions + 2 x other VALU instructions)
+                    / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
+                  issue cycles of the VALU instructions (wave64 on a SIMD: 2 cycles, f64 at half rate:
+                  4) over the SIMD cycles of the dispatch -- the bench's formula (bench.py roofline)
+  valu_active_frac = 4 x SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
+                  cycles waves spent issuing VALU (summed over waves) over the SIMD cycles
+  wave_wait_frac  = SQ_WAIT_ANY / SQ_WAVE_CYCLES
 
-    python tools/pmc_summary.py gpurun_out/pmc_a gpurun_out/pmc_b ... --out profiles/r02_counters_X.json
+    python tools/pmc_summary.py gpurun_out/pmc_a gpurun_out/pmc_b ... --out profiles/r03_counters_X.json
+    python tools/pmc_summary.py --recompute profiles/r02_counters_X.json ...   (derived fields again
+                                                                                 from stored counters)
 """
 import argparse
 import csv
@@ -23,6 +32,8 @@ import os
 from collections import defaultdict
 
 CUS = 256
+SIMDS = 4 * CUS
+XCDS = 8
 
 
 def short(name):
@@ -42,12 +53,59 @@ def load(dirpath):
     return per
 
 
+DERIVED = {"traffic_bytes": "2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024",
+           "fp64_flop": "64 x (SQ_INSTS_VALU_ADD_F64 + MUL_F64 + TRANS_F64 + 2 x FMA_F64)",
+           "valu_issue_frac": "(4 x f64 VALU insts + 2 x other VALU insts) / (GRBM_GUI_ACTIVE / %d XCDs x %d SIMDs)"
+                              % (XCDS, SIMDS),
+           "valu_active_frac": "4 x SQ_ACTIVE_INST_VALU (quad-cycles) / (GRBM_GUI_ACTIVE / %d XCDs x %d SIMDs)"
+                               % (XCDS, SIMDS),
+           "wave_wait_frac": "SQ_WAIT_ANY / SQ_WAVE_CYCLES"}
+
+
+def derive(c):
+    """Derived per-launch figures from the counter means `c`."""
+    rec = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rec["fetch_bytes"] = 2 * c["FETCH_SIZE"] * 1024
+        rec["write_bytes"] = c["WRITE_SIZE"] * 1024
+        rec["traffic_bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
+    f64 = [c.get("SQ_INSTS_VALU_%s_F64" % op) for op in ("ADD", "MUL", "TRANS", "FMA")]
+    if all(v is not None for v in f64):
+        rec["fp64_flop"] = 64 * (f64[0] + f64[1] + f64[2] + 2 * f64[3])
+    cyc = c.get("GRBM_GUI_ACTIVE", 0) / XCDS * SIMDS
+    if cyc and "SQ_INSTS_VALU" in c and all(v is not None for v in f64[:2]) and f64[3] is not None:
+        n64 = f64[0] + f64[1] + f64[3]
+        rec["valu_issue_frac"] = (4 * n64 + 2 * (c["SQ_INSTS_VALU"] - n64)) / cyc
+    if cyc and "SQ_ACTIVE_INST_VALU" in c:
+        rec["valu_active_frac"] = 4 * c["SQ_ACTIVE_INST_VALU"] / cyc
+    if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
+        rec["wave_wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    return rec
+
+
+def recompute(paths):
+    for p in paths:
+        out = json.load(open(p))
+        out["derived"] = DERIVED
+        for k, rec in out["kernels"].items():
+            for key in ("valu_issue_frac", "valu_active_frac", "wave_wait_frac"):
+                rec.pop(key, None)
+            rec.update(derive(rec["counters"]))
+        with open(p, "w") as fh:
+            json.dump(out, fh, indent=1)
+        print(p, {k: (round(r.get("valu_issue_frac", -1), 4), round(r.get("valu_active_frac", -1), 4))
+                  for k, r in out["kernels"].items() if "k_primary" in k or "k_frame" in k or "k_trace" in k})
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("dirs", nargs="+")
-    ap.add_argument("--out", required=True)
+    ap.add_argument("dirs", nargs="*")
+    ap.add_argument("--out")
     ap.add_argument("--label", default="")
+    ap.add_argument("--recompute", nargs="+", help="summary files whose derived fields are recomputed")
     a = ap.parse_args()
+    if a.recompute:
+        return recompute(a.recompute)
     merged = defaultdict(dict)
     launches = defaultdict(dict)
     for d in a.dirs:
@@ -56,22 +114,11 @@ def main():
                 merged[k][c] = sum(vals) / len(vals)
                 launches[k][c] = len(vals)
     out = {"label": a.label, "units": "per launch (mean over the launches of each pass)", "passes": a.dirs,
-           "derived": {"traffic_bytes": "2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024",
-                       "fp64_flop": "64 x (SQ_INSTS_VALU_ADD_F64 + MUL_F64 + TRANS_F64 + 2 x FMA_F64)",
-                       "valu_issue_frac": "SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE x %d CUs x 4 SIMDs)" % CUS},
-           "kernels": {}}
+           "derived": DERIVED, "kernels": {}}
     for k in sorted(merged):
         c = merged[k]
         rec = {"counters": c, "launches": launches[k]}
-        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            rec["fetch_bytes"] = 2 * c["FETCH_SIZE"] * 1024
-            rec["write_bytes"] = c["WRITE_SIZE"] * 1024
-            rec["traffic_bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
-        f64 = [c.get("SQ_INSTS_VALU_%s_F64" % op) for op in ("ADD", "MUL", "TRANS", "FMA")]
-        if all(v is not None for v in f64):
-            rec["fp64_flop"] = 64 * (f64[0] + f64[1] + f64[2] + 2 * f64[3])
-        if "SQ_ACTIVE_INST_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
-            rec["valu_issue_frac"] = c["SQ_ACTIVE_INST_VALU"] / (c["GRBM_GUI_ACTIVE"] * CUS * 4)
+        rec.update(derive(c))
         out["kernels"][k] = rec
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
