@@ -367,6 +367,8 @@ def main():
                          "slowest rank, value = all ranks' rays / that time)")
     ap.add_argument("--shard-bands", type=int, default=0,
                     help="most row bands per rank (library option shard_bands; default rt_device.h SHARD_BANDS)")
+    ap.add_argument("--shard-snake", type=int, default=-1,
+                    help="band dealing order, 0 round-robin / 1 snake (library option shard_snake; default SHARD_SNAKE)")
     args = ap.parse_args()
 
     cmd = launch_plan(args.gpus, os.environ, visible_gpus() if "WORLD_SIZE" not in os.environ and args.gpus > 1
@@ -411,6 +413,8 @@ def main():
     N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))  # size every frame slot during the warmup
     if args.shard_bands:
         N.check(lib, lib.srt_set_option(ctx, b"shard_bands", args.shard_bands))
+    if args.shard_snake >= 0:
+        N.check(lib, lib.srt_set_option(ctx, b"shard_snake", args.shard_snake))
     for kv in args.option:
         k, v = kv.split("=")
         N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
@@ -419,13 +423,15 @@ def main():
     npix_full = W * H
     flags = N.RENDER_SHARDED | N.RENDER_RGB_ROWS if world > 1 else 0
     rows32 = None
-    from sightpy._shard import SHARD_BANDS, band_height, shard_rows
+    from sightpy._shard import SHARD_BANDS, SHARD_SNAKE, band_height, shard_rows
 
     kmax = args.shard_bands or SHARD_BANDS
+    snake = args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE
     rehearse = {None: None}  # rank -> its rows (None: the frame as the launcher splits it)
     if args.shard_of > 1 and world == 1:
         ranks = range(args.shard_of) if args.shard_rank == "all" else [int(args.shard_rank)]
-        rehearse = {r: np.ascontiguousarray(shard_rows(H, args.shard_of, r, kmax), dtype=np.int32) for r in ranks}
+        rehearse = {r: np.ascontiguousarray(shard_rows(H, args.shard_of, r, kmax, snake), dtype=np.int32)
+                    for r in ranks}
         rows32 = rehearse[min(ranks)]
         npix_full = max(len(v) for v in rehearse.values()) * W  # the shards' outputs
 
@@ -580,7 +586,8 @@ def main():
                                 "-> sRGB resolve -> uint8 + linear RGB (f64) in pinned host memory; frames pipelined",
                        "frame_ms": round(ms_step, 4),
                        "host_enqueue_ms": round(max(enq), 4),
-                       "row_bands": {"kmax": kmax, "band_height": band_height(H, max(world, args.shard_of, 1), kmax)}},
+                       "row_bands": {"kmax": kmax, "snake": snake,
+                                     "band_height": band_height(H, max(world, args.shard_of, 1), kmax, snake)}},
         }
         if len(rehearse) > 1:
             rec["rank_frame_ms"] = [round(x, 4) for x in rank_ms]
@@ -599,7 +606,7 @@ def main():
                 pmc_counters(args.config, kname)
             from sightpy._shard import shard_rows
 
-            npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0)) * W
+            npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0, kmax, snake)) * W
             st_pass = dict(st0[0])
             st_pass["rays_per_depth"] = [r / npass for r in st0[0]["rays_per_depth"]]
             model = kernel_bytes_model(st_pass, spp / npass, npix_rank, sc.camera.lens_radius != 0.0)

@@ -61,7 +61,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 832;
+constexpr size_t TRACE_PARAMS_BYTES = 848;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
@@ -117,6 +117,11 @@ struct TraceParams {
     const int32_t* force_id;
     const double* force_t;
     const double* force_o;
+    // k_frame sample groups: block b takes tile b % ntiles and the samples [g spg, (g+1) spg) of the
+    // pass, g = b / ntiles; groups > 1 store their partial sums to fbg[g][3][npix] (k_fb_groups adds them)
+    double* fbg;
+    int groups;
+    int ntiles;
 };
 // kernel argument: host and device passes must agree on the layout (catches address-space pointer
 // size differences, see SceneView)
@@ -243,6 +248,13 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* ctr, uint32_t cnt) {
     return base + below;
 }
 
+// the exclusive prefix of `cnt` over the active lanes below this one (wave_reserve's `below`)
+__device__ __forceinline__ uint32_t wave_below(uint32_t cnt) {
+    uint32_t below = 0;
+    for (int b = 0; b < 8; ++b) below += lanes_below(__ballot((cnt >> b) & 1u)) << b;
+    return below;
+}
+
 // Emitter of the GPU trace step: colour -> framebuffer atomics, children -> output queue shard.
 struct GpuEmit {
     const TraceParams& P;
@@ -276,14 +288,23 @@ struct GpuEmit {
         uint32_t slot = wave_reserve(P.cnt_out + shard, 1u);
         store(slot, c, child_path(r.path, c.slot, round));
     }
+    // the fan-out child-major: the k-th children of the wave's lanes take consecutive slots, so every
+    // store of a child is one coalesced run (lane-major slots scattered each store over 64 lines)
     __device__ void diffuse(const DiffuseGen& g, int mi) const {
-        uint32_t slot = wave_reserve(P.cnt_out + shard, (uint32_t)g.count);
+        const uint32_t cnt = (uint32_t)g.count;
+        const uint32_t base = wave_reserve(P.cnt_out + shard, cnt) - wave_below(cnt);
         const auto& m = P.S.mat[mi];
-        for (int k = 0; k < g.count; ++k) {
-            Rng rng;
-            const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
-            store(slot + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
+        uint32_t off = 0;
+        for (uint32_t k = 0;; ++k) {
+            const uint64_t mk = __ballot(cnt > k);
+            if (!mk) break;
+            if (cnt > k) {
+                Rng rng;
+                const uint32_t cpath = child_path(r.path, 0x100u + k, round);
+                rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
+                store(base + off + lanes_below(mk), diffuse_child(P.S, m, g, rng, k), cpath);
+            }
+            off += (uint32_t)__builtin_popcountll(mk);
         }
     }
 };
@@ -708,14 +729,25 @@ struct FrameEmit {
     __device__ void child(const Child& c) const {
         store(reserve(1u), c, child_path(r.path, c.slot, round));
     }
+    // the fan-out child-major in the ring (as GpuEmit::diffuse): the k-th children of the lanes are
+    // consecutive, every store a coalesced run.  Lane-major positions scattered each store over 64
+    // cache lines and doubled the ring's HBM writes (cornell k_frame: 309 GB written per pass for
+    // 143 GB of rays, PMC WRITE_SIZE)
     __device__ void diffuse(const DiffuseGen& g, int mi) const {
-        const uint32_t pos = reserve((uint32_t)g.count);
+        const uint32_t cnt = (uint32_t)g.count;
+        const uint32_t base = reserve(cnt) - wave_below(cnt);
         const auto& m = P.S.mat[mi];
-        for (int k = 0; k < g.count; ++k) {
-            Rng rng;
-            const uint32_t cpath = child_path(r.path, 0x100u + (uint32_t)k, round);
-            rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
-            store(pos + (uint32_t)k, diffuse_child(P.S, m, g, rng, (uint32_t)k), cpath);
+        uint32_t off = 0;
+        for (uint32_t k = 0;; ++k) {
+            const uint64_t mk = __ballot(cnt > k);
+            if (!mk) break;
+            if (cnt > k) {
+                Rng rng;
+                const uint32_t cpath = child_path(r.path, 0x100u + k, round);
+                rng.init(P.seed, key_pix(P, r.pix), cpath, 0xD1000000u | meta_depth(r.meta));
+                store(base + off + lanes_below(mk), diffuse_child(P.S, m, g, rng, k), cpath);
+            }
+            off += (uint32_t)__builtin_popcountll(mk);
         }
     }
 };
@@ -745,7 +777,10 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     }
     __syncthreads();
     RT_ACC(18, tf0);
-    const uint32_t tile0 = blockIdx.x * FRAME_BLOCK;
+    const uint32_t tile = blockIdx.x % (uint32_t)P.ntiles, grp = blockIdx.x / (uint32_t)P.ntiles;
+    const uint32_t tile0 = tile * FRAME_BLOCK;
+    const int spg = (P.spp + P.groups - 1) / P.groups;
+    const int s_end = min(P.spp, (int)(grp + 1) * spg);
     const int64_t ring_base = (int64_t)L.slot * P.ring_cap;
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
@@ -759,16 +794,16 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
     const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
     const Quot qw((double)P.cam.width), qh((double)P.cam.height);
-    int s_next = 0;
+    int s_next = (int)grp * spg;
     for (;;) {
         const uint32_t head = lds_get(&L.head), tail = lds_get(&L.tail);
         const uint32_t pending = tail - head;
-        if (pending == 0u && s_next >= P.spp) break;
+        if (pending == 0u && s_next >= s_end) break;
         Ray r;
         bool active;
         uint32_t depth = 0;
         int32_t* hs = nullptr;
-        if (pending >= (uint32_t)FRAME_BLOCK || s_next >= P.spp) {
+        if (pending >= (uint32_t)FRAME_BLOCK || s_next >= s_end) {
             // a chunk of the ring
             const uint32_t take = min(pending, (uint32_t)FRAME_BLOCK);
             active = lane < take;
@@ -826,6 +861,9 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             const int64_t p0 = p - lane;
             store_u8_chunk(P.out_u8 + 3 * p0, px, lane, (int)min<int64_t>(64, P.npix - p0));
         }
+    } else if (pact && P.groups > 1) {
+        double* part = P.fbg + (int64_t)grp * 3 * P.npix;
+        part[p] = L.acc[0][lane]; part[P.npix + p] = L.acc[1][lane]; part[2 * P.npix + p] = L.acc[2][lane];
     } else if (pact) {
         const double ar = L.acc[0][lane], ag = L.acc[1][lane], ab = L.acc[2][lane];
         if (P.fb_first) {
@@ -973,6 +1011,15 @@ __global__ __launch_bounds__(BLOCK) void k_fx_combine(double* fb, const unsigned
     if (bad) atomicOr(flags + 1, RETRY_FIXED_RANGE);
 }
 
+// the sample groups' partial sums of a frame-kernel pass into the framebuffer, in group order
+__global__ __launch_bounds__(BLOCK) void k_fb_groups(double* fb, const double* fbg, int groups, int64_t npix, int first) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < 3 * npix; i += (int64_t)gridDim.x * BLOCK) {
+        double v = fbg[i];
+        for (int g = 1; g < groups; ++g) v += fbg[(int64_t)g * 3 * npix + i];
+        fb[i] = first ? v : fb[i] + v;
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_nearest(SceneView S, const double* O, const double* D, int64_t n, double* t,
                                                   int32_t* id, double* orient) {
     for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
@@ -1056,12 +1103,12 @@ struct GatherTiles {
     int64_t npix[MAX_RANKS];       // rows_q * W
 };
 
-__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t band, int64_t W, int64_t H,
-                                                   uint8_t* u8, double* rgb) {
+__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t band, int snake, int64_t W,
+                                                   int64_t H, uint8_t* u8, double* rgb) {
     const int64_t n = W * H;
     for (int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x; g < n; g += (int64_t)gridDim.x * BLOCK) {
         const int64_t y = g / W, x = g - y * W;
-        const int q = shard_of_row(y, nranks, band);
+        const int q = shard_of_row(y, nranks, band, snake);
         const int64_t l = shard_local_row(y, nranks, band) * W + x;
         if (u8) {
             const uint8_t* s = T.u8[q] + 3 * l;
@@ -1075,10 +1122,10 @@ __global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, i
     }
 }
 
-std::vector<int32_t> band_rows(int64_t H, int n, int q, int64_t band) {
+std::vector<int32_t> band_rows(int64_t H, int n, int q, int64_t band, int snake) {
     std::vector<int32_t> r;
     for (int64_t y = 0; y < H; ++y)
-        if (shard_of_row(y, n, band) == q) r.push_back((int32_t)y);
+        if (shard_of_row(y, n, band, snake) == q) r.push_back((int32_t)y);
     return r;
 }
 
@@ -1117,6 +1164,7 @@ struct FramePlan {
     int64_t W = 0, H = 0;  // frame shape (a shard renders npix of W * H)
     bool sharded = false, gather_rgb = false, use_mt = false;
     int spp = 0, batch = 0, npass = 0, dcap = 0, nev = 0;
+    int groups = 1;  // k_frame sample groups per tile (the largest pass's)
     int64_t cnt_words = 0, pass_words = 0;
 };
 
@@ -1152,6 +1200,8 @@ struct FrameSlot {
     // frame buffers
     double* fb = nullptr;
     int64_t fb_cap = 0;
+    double* fbg = nullptr;  // k_frame sample groups' partial sums [groups][3][npix]
+    int64_t fbg_cap = 0;
     unsigned long long* fbx = nullptr;  // [3][npix] fixed-point sums + [npix] f32 magnitudes (fb_add)
     int64_t fbx_cap = 0;
     double* rgb = nullptr;
@@ -1181,6 +1231,7 @@ struct FrameSlot {
     struct Gather {
         bool on = false;
         int64_t W = 0, H = 0, npix = 0, maxpix = 0, band = 1;
+        int snake = 0;
         bool want_u8 = false, want_rgb = false;
         uint8_t* dst_u8 = nullptr;  // where k_assemble writes (caller's device buffer or full_u8)
         double* dst_rgb = nullptr;
@@ -1292,6 +1343,8 @@ struct srt_ctx {
     bool defer_gather = false;  // srt_render_group posts the gathers of all its contexts in one group
     bool retry_frame = false;   // the last finish_async failed only with RETRY_* bits (render the frame again)
     int shard_bands = SHARD_BANDS;  // option "shard_bands": most row bands per rank (rt_device.h shard_band_height)
+    int shard_snake = SHARD_SNAKE;  // option "shard_snake": bands dealt in alternating direction per period
+    int frame_groups = 0;           // option "frame_groups": k_frame sample groups per tile (0: auto)
     double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
@@ -1791,7 +1844,7 @@ void free_slot(FrameSlot& f) {
     (void)hipStreamSynchronize(f.stream);
     free_list(f.queue_bufs);
     free_list(f.ring_bufs);
-    void* bufs[] = {f.fb, f.fbx, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb,
+    void* bufs[] = {f.fb, f.fbg, f.fbx, f.rgb, f.u8, f.jit, f.hit, f.counts, f.flags, f.shadow, f.g_u8, f.g_rgb, f.full_u8, f.full_rgb,
                     f.mt_win};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -1863,7 +1916,9 @@ int finish_async(srt_ctx* c, srt_stats* st) {
     return SRT_OK;
 }
 
-int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) { return shard_rank_rows(G.H, nranks, q, G.band) * G.W; }
+int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) {
+    return shard_rank_rows(G.H, nranks, q, G.band, G.snake) * G.W;
+}
 
 // Post this rank's part of the frame's gather on its stream (inside an RCCL group): rank 0 receives
 // every other rank's uint8 (and linear-RGB) tile, the others send theirs.
@@ -1909,7 +1964,7 @@ int gather_finish(srt_ctx* c) {
         T.npix[q] = shard_npix(G, c->nranks, q);
     }
     hipStream_t st = c->f->stream;
-    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.band, G.W, G.H,
+    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.band, G.snake, G.W, G.H,
                        G.want_u8 ? G.dst_u8 : nullptr, G.want_rgb ? G.dst_rgb : nullptr);
     HIP_TRY(hipGetLastError());
     if (G.host_u8) HIP_TRY(hipMemcpyAsync(G.host_u8, G.dst_u8, (size_t)3 * G.W * G.H, hipMemcpyDeviceToHost, st));
@@ -1985,6 +2040,15 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "frame_groups")) {
+        if (value < 0 || value > 4096) return fail(SRT_ERR_ARG, "frame_groups: 0 (auto) .. 4096");
+        c->frame_groups = (int)value;
+        return SRT_OK;
+    }
+    if (!strcmp(key, "shard_snake")) {
+        c->shard_snake = value != 0;
+        return SRT_OK;
+    }
     if (!strcmp(key, "shard_bands")) {
         if (value < 1 || value > 4096) return fail(SRT_ERR_ARG, "shard_bands: 1..4096");
         c->shard_bands = (int)value;
@@ -2186,8 +2250,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (c->nranks > MAX_RANKS) return fail(SRT_ERR_ARG, "too many ranks");
         if (cam->height < c->nranks) return fail(SRT_ERR_ARG, "a sharded frame needs at least one row per rank");
         if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
-        band = shard_band_height(cam->height, c->nranks, c->shard_bands);
-        rows_h = band_rows(cam->height, c->nranks, c->rank, band);
+        band = shard_band_height(cam->height, c->nranks, c->shard_bands, c->shard_snake);
+        rows_h = band_rows(cam->height, c->nranks, c->rank, band, c->shard_snake);
         n_rows = (int)rows_h.size();
         rows_src = rows_h.data();
     } else if (a->rows) {
@@ -2242,6 +2306,16 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     F.cnt_words = (int64_t)SRT_MAX_DEPTHS * NSHARD;
     F.pass_words = F.cnt_words + 2;
     F.frame = c->use_frame < 0 ? c->fanout > 1 : c->use_frame != 0;
+    const int64_t ntiles = (npix + FRAME_BLOCK - 1) / FRAME_BLOCK;
+    if (F.frame) {
+        // a frame kernel block traces one 64-pixel tile through the pass's samples: a small frame (a
+        // shard of a multi-GPU frame) has too few tiles to fill the GPU, so its samples are split
+        // into groups, one block per (tile, group), until there are ~4 blocks per resident wave
+        // slot (c->max_blocks = 8 per CU at 2 waves/SIMD)
+        const int64_t want = 4 * (int64_t)c->max_blocks;
+        const int64_t g = c->frame_groups > 0 ? c->frame_groups : (want + ntiles - 1) / ntiles;
+        F.groups = (int)std::max<int64_t>(1, std::min<int64_t>(g, batch));
+    }
     if (!F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
         c->hint_key[2] == batch) {
         for (int d = 1; d <= F.dcap; ++d)
@@ -2282,7 +2356,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!mt_bt[0] || !mt_bt[1]) mt_bt[0] = mt_bt[1] = nullptr;
     }
     const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * W * Hf : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
-    const int64_t maxpix = sharded ? shard_rank_rows(Hf, c->nranks, 0, band) * W : 0;  // rank 0 has the most rows
+    const int64_t maxpix = sharded ? shard_max_rows(Hf, c->nranks, band, c->shard_snake) * W : 0;  // the gather's tile
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
     // for them (and reports their errors)
     if (async && c->async_pending > 0) {
@@ -2294,6 +2368,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
                           (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
                           F.frame == pp.frame && F.chain_from == pp.chain_from && F.W == pp.W && F.H == pp.H &&
+                          F.groups == pp.groups && (F.groups == 1 || (int64_t)F.groups * 3 * npix <= c->f->fbg_cap) &&
                           F.sharded == pp.sharded && F.gather_rgb == pp.gather_rgb && F.use_mt == pp.use_mt &&
                           (!sharded || c->rank != 0 ||
                            (c->f->g_u8_cap >= c->nranks * maxpix * 3 && c->f->full_u8_cap >= 3 * W * Hf &&
@@ -2326,6 +2401,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         c->f = &fs;
         int r = SRT_OK;
         if (!r) r = ensure_buf(&c->f->fb, c->f->fb_cap, 3 * npix);
+        if (!r && F.groups > 1) r = ensure_buf(&c->f->fbg, c->f->fbg_cap, (int64_t)F.groups * 3 * npix);
         if (!r) r = ensure_buf(&c->f->fbx, c->f->fbx_cap, fx_words(npix));
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
@@ -2514,16 +2590,24 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 P.nslot = c->f->nslot;
                 P.dcap = F.dcap;
                 P.cnt_out = c->f->counts;
-                P.fuse_resolve = (F.npass == 1);
+                P.groups = std::min(F.groups, ns);
+                P.ntiles = (int)ntiles;
+                P.fbg = c->f->fbg;
+                P.fuse_resolve = (F.npass == 1 && F.groups == 1);
                 P.out_rgb = res_rgb;
                 P.out_u8 = res_u8;
                 P.spp_total = a->spp;
                 // (the fused resolve rewrites rgb / u8: the previous frame's copies from them first)
                 if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
                 HIP_TRY(hipEventRecord(ev[0], c->f->stream));
-                hipLaunchKernelGGL(V.frame, dim3((unsigned)((npix + FRAME_BLOCK - 1) / FRAME_BLOCK)), dim3(FRAME_BLOCK),
-                                   lut_bytes(c), c->f->stream, P);
+                hipLaunchKernelGGL(V.frame, dim3((unsigned)(ntiles * P.groups)), dim3(FRAME_BLOCK), lut_bytes(c),
+                                   c->f->stream, P);
                 HIP_TRY(hipGetLastError());
+                if (P.groups > 1) {
+                    hipLaunchKernelGGL(k_fb_groups, dim3(grid_for(3 * npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream,
+                                       c->f->fb, (const double*)c->f->fbg, P.groups, npix, (int)P.fb_first);
+                    HIP_TRY(hipGetLastError());
+                }
                 HIP_TRY(hipEventRecord(ev[1], c->f->stream));
                 HIP_TRY(hipEventRecord(ev[F.dcap + 1], c->f->stream));
                 if (mst != c->f->stream) {  // the next generation into this slot may start
@@ -2577,7 +2661,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (use_mt) c->mt_pos = mt_pos;
         uint32_t* hshadow = c->f->host + F.npass * F.pass_words;
         // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
-        const bool fused = F.frame && F.npass == 1;
+        const bool fused = F.frame && F.npass == 1 && F.groups == 1;
         uint32_t* hlast = c->f->host + (F.npass - 1) * F.pass_words;
         if (c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
         hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
@@ -2587,22 +2671,31 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
         c->f->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
-        // this rank's rows of the linear RGB into the shared host frame: per plane, the full bands as
-        // one pitched copy (the rank's band b is frame rows band (b nranks + rank) ..), then a short
-        // last band
+        // this rank's rows of the linear RGB into the shared host frame: per plane and per class of
+        // bands with one frame-row stride (round-robin: all of them, a rank's band j at frame band
+        // j n + rank; snake: even and odd j), one pitched copy of the full bands, then a short last band
         if (rgb_rows) {
             const int64_t band_px = band * W;
             const int64_t nb = npix / band_px, tail = npix - nb * band_px;
+            const int step = c->shard_snake ? 2 : 1;
             for (int pl = 0; pl < 3; ++pl) {
                 double* dst = a->out_rgb + (int64_t)pl * W * Hf;
                 const double* src = c->f->rgb + (int64_t)pl * npix;
-                if (nb > 0)
-                    HIP_TRY(hipMemcpy2DAsync(dst + (int64_t)c->rank * band_px, (size_t)(c->nranks * band_px * 8), src,
-                                             (size_t)(band_px * 8), (size_t)(band_px * 8), (size_t)nb,
-                                             hipMemcpyDeviceToHost, c->f->stream));
-                if (tail > 0)
-                    HIP_TRY(hipMemcpyAsync(dst + (nb * c->nranks + c->rank) * band_px, src + nb * band_px,
-                                           (size_t)(tail * 8), hipMemcpyDeviceToHost, c->f->stream));
+                for (int cls = 0; cls < step; ++cls) {
+                    const int64_t cnt = nb > cls ? (nb - cls + step - 1) / step : 0;
+                    if (cnt == 0) continue;
+                    const int64_t b0 = (int64_t)cls * c->nranks + (c->shard_snake && (cls & 1) ? c->nranks - 1 - c->rank
+                                                                                                 : c->rank);
+                    HIP_TRY(hipMemcpy2DAsync(dst + b0 * band_px, (size_t)(step * c->nranks * band_px * 8),
+                                             src + cls * band_px, (size_t)(step * band_px * 8), (size_t)(band_px * 8),
+                                             (size_t)cnt, hipMemcpyDeviceToHost, c->f->stream));
+                }
+                if (tail > 0) {
+                    // (the rank's band nb, in period nb)
+                    const int64_t bt = nb * c->nranks + ((c->shard_snake && (nb & 1)) ? c->nranks - 1 - c->rank : c->rank);
+                    HIP_TRY(hipMemcpyAsync(dst + bt * band_px, src + nb * band_px, (size_t)(tail * 8),
+                                           hipMemcpyDeviceToHost, c->f->stream));
+                }
             }
         }
         // the shard's tiles to rank 0 (RCCL over xGMI), assembled into the frame there
@@ -2615,6 +2708,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             G.npix = npix;
             G.maxpix = maxpix;
             G.band = band;
+            G.snake = c->shard_snake;
             G.want_u8 = true;
             G.want_rgb = gather_rgb;
             if (c->rank == 0) {

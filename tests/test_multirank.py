@@ -40,7 +40,7 @@ def test_shard_rows_partition():
             parts = [shard_rows(H, world, r) for r in range(world)]
             allrows = np.sort(np.concatenate(parts))
             assert np.array_equal(allrows, np.arange(H))
-            assert max(len(p) for p in parts) == max_shard_rows(H, world) == len(parts[0])
+            assert max(len(p) for p in parts) == max_shard_rows(H, world)
             idx = assemble_index(H, world)
             buf = np.full(world * max_shard_rows(H, world), -1)
             for r, p in enumerate(parts):
@@ -57,35 +57,40 @@ def test_shard_rows_partition():
     assert band_height(800, 8) == 20 and [len(shard_rows(800, 8, r)) for r in range(8)] == [100] * 8
     # one band per rank allowed: contiguous blocks
     assert band_height(1080, 8, kmax=1) == 135
+    # snake order: period 1 is dealt backwards
+    assert list(shard_rows(40, 2, 0, kmax=2, snake=1)) == list(range(0, 10)) + list(range(30, 40))
+    assert list(shard_rows(40, 2, 0, kmax=2, snake=0)) == list(range(0, 10)) + list(range(20, 30))
 
 
-def _kernel_shard_map(H, n, kmax=8):
+def _kernel_shard_map(H, n, kmax=8, snake=1):
     import hostcheck as HC
 
     owner = np.empty(H, dtype=np.int32)
     local = np.empty(H, dtype=np.int64)
     lib = HC.lib()
-    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                 ctypes.c_void_p]
     lib.hc_shard_map.restype = ctypes.c_int64
-    h = lib.hc_shard_map(H, n, kmax, owner.ctypes.data, local.ctypes.data)
+    h = lib.hc_shard_map(H, n, kmax, snake, owner.ctypes.data, local.ctypes.data)
     return owner, local, h
 
 
 @pytest.mark.parametrize("H", [8, 37, 300, 800, 1080, 2160])
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("kmax", [1, 4, 8, 17])
-def test_kernel_shard_map_matches_partition(H, n, kmax):
+@pytest.mark.parametrize("snake", [0, 1])
+def test_kernel_shard_map_matches_partition(H, n, kmax, snake):
     from sightpy._shard import shard_rows, band_height, rank_rows
 
-    owner, local, h = _kernel_shard_map(H, n, kmax)
-    assert h == band_height(H, n, kmax)
+    owner, local, h = _kernel_shard_map(H, n, kmax, snake)
+    assert h == band_height(H, n, kmax, snake)
     for q in range(n):
-        rows = shard_rows(H, n, q, kmax)
-        assert len(rows) == rank_rows(H, n, q, h)
+        rows = shard_rows(H, n, q, kmax, snake)
+        assert len(rows) == rank_rows(H, n, q, h, snake)
         assert np.array_equal(np.where(owner == q)[0], rows)
         assert np.array_equal(local[rows], np.arange(len(rows)))
-    # rank 0 holds the most rows (the gather pads every tile to its size)
-    assert max(len(shard_rows(H, n, q, kmax)) for q in range(n)) == len(shard_rows(H, n, 0, kmax))
+        # a rank's j-th band lies in period j (the RGB row copies and the local-row map rely on it)
+        assert np.array_equal(rows // (h * n), np.arange(len(rows)) // h)
 
 
 def _gather_worker(rank, world, port, H, W):
@@ -94,7 +99,7 @@ def _gather_worker(rank, world, port, H, W):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
-    from sightpy._shard import shard_rows
+    from sightpy._shard import shard_rows, max_shard_rows
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     full = np.random.default_rng(7).integers(0, 256, size=(H, W, 3), dtype=np.uint8)
@@ -103,7 +108,7 @@ def _gather_worker(rank, world, port, H, W):
     tile_u8 = full[rows].copy()
     tile_rgb = rgb.reshape(3, H, W)[:, rows].reshape(3, -1).copy()
     if rank == 0:
-        maxpix = len(shard_rows(H, world, 0)) * W
+        maxpix = max_shard_rows(H, world) * W
         g_u8 = np.zeros((world, maxpix * 3), dtype=np.uint8)
         g_rgb = np.zeros((world, 3 * maxpix))
         g_u8[0, : tile_u8.size] = tile_u8.reshape(-1)
@@ -258,8 +263,8 @@ def test_gpu_every_shard_of_an_n_rank_frame_assembles_to_the_plain_render(world)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world):
+@pytest.mark.parametrize("world,kmax,snake", [(2, 8, 1), (3, 8, 0), (3, 8, 1), (3, 3, 1), (8, 2, 1), (8, 17, 0)])
+def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax, snake):
     """SRT_RENDER_RGB_ROWS (the multi-GPU bench's output path): each rank writes its own rows of the
     linear RGB into one host frame with pitched copies.  Rehearsed on one card (option
     rehearse_shard: act as rank r of N without a communicator): the N shards, rendered in turn into
@@ -268,6 +273,7 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world):
 
     import scenes
     from sightpy import _backend as B, _native as N
+    from sightpy._shard import SHARD_BANDS, SHARD_SNAKE
 
     W, H, spp = 120, 70, 2  # 70 rows: a short last band
     sc = scenes.example1(W, H, 4)
@@ -278,6 +284,8 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world):
     cd = B.camera_desc(sc.camera)
     host = ctypes.c_void_p()
     N.check(lib, lib.srt_host_alloc(ctx, 3 * W * H * 8, ctypes.byref(host)))
+    N.check(lib, lib.srt_set_option(ctx, b"shard_bands", kmax))
+    N.check(lib, lib.srt_set_option(ctx, b"shard_snake", snake))
     try:
         frame = np.ctypeslib.as_array((ctypes.c_double * (3 * W * H)).from_address(host.value))
         frame[:] = np.nan
@@ -298,6 +306,8 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world):
         assert np.array_equal(frame.reshape(3, -1), full.rgb)
     finally:
         lib.srt_set_option(ctx, b"rehearse_shard", 0)
+        lib.srt_set_option(ctx, b"shard_bands", SHARD_BANDS)
+        lib.srt_set_option(ctx, b"shard_snake", SHARD_SNAKE)
         lib.srt_host_free(ctx, host)
 
 
