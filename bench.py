@@ -240,7 +240,7 @@ def roofline(kname, kms, model_bytes, frame_path, krec, src):
     if krec.get("wave_wait_frac") is not None:
         roof["wave_wait_frac"] = round(krec["wave_wait_frac"], 4)
     if "valu_issue_frac" in roof and "wave_wait_frac" in roof:
-        roof["limiter"] = ("latency: 2 waves/SIMD (register-bound); waves wait on memory %.0f%% of their cycles, VALU "
+        roof["limiter"] = ("latency: 3 waves/SIMD (168 VGPRs); waves wait on memory %.0f%% of their cycles, VALU "
                            "issue %.0f%% busy, HBM %.0f%% of peak" % (100 * roof["wave_wait_frac"],
                                                                     100 * roof["valu_issue_frac"],
                                                                     100 * roof["traffic_frac"]))

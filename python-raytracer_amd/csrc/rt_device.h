@@ -346,6 +346,20 @@ RT_HD double collider_hit(const RT_RO srt_collider& c, d3 O, d3 D, double& o) {
     }
 }
 
+// Large libm routines called only on rare paths (the Glossy lobe's non-integer power, sphere uv)
+// are kept out of line: inlined, their temporaries set the register allocation of every shading
+// kernel (k_primary<33> at 3 waves/SIMD: 127 VGPRs spilled inlined, none out of line); the call
+// returns the same value as the inlined routine
+#ifdef __HIP_DEVICE_COMPILE__
+__device__ __attribute__((noinline)) double pow_ool(double x, double y) { return pow(x, y); }
+__device__ __attribute__((noinline)) double atan2_ool(double y, double x) { return atan2(y, x); }
+__device__ __attribute__((noinline)) double asin_ool(double x) { return asin(x); }
+#else
+inline double pow_ool(double x, double y) { return pow(x, y); }
+inline double atan2_ool(double y, double x) { return atan2(y, x); }
+inline double asin_ool(double x) { return asin(x); }
+#endif
+
 // ---- normals and uv (per collider) ---------------------------------------------------------
 // cuboid.py:142-151: face normal picked by the largest scaled |local coordinate|
 RT_HD d3 cuboid_normal(const RT_RO double* p, d3 P) {
@@ -399,8 +413,8 @@ RT_HD bool collider_uv(const RT_RO srt_collider& c, d3 P, double& u, double& v) 
     switch (c.type) {
         case SRT_SPHERE: {  // sphere.py:58-64
             d3 M = divs(sub(P, ld3(c.p)), c.p[3]);
-            u = (atan2(M.z, M.x) + PI) / TWO_PI;
-            v = (asin(M.y) + HALF_PI) / PI;
+            u = (atan2_ool(M.z, M.x) + PI) / TWO_PI;
+            v = (asin_ool(M.y) + HALF_PI) / PI;
             break;
         }
         case SRT_PLANE: {  // plane.py:98-102
@@ -807,7 +821,7 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
 #else
             RT_T0(tp0);
             const double nh = np_clip(dot(N, H), 0.0, 1.0);
-            double Dphong = ((m.ival > 0 ? powi(nh, m.ival) : pow(nh, m.p[4])) * m.p[5]) / m.p[6];
+            double Dphong = ((m.ival > 0 ? powi(nh, m.ival) : pow_ool(nh, m.p[4])) * m.p[5]) / m.p[6];
             RT_ACC(6, tp0);
 #endif
             double den = 4.0 * np_clip(dot(N, V) * NdotL, 0.001, 1.0);

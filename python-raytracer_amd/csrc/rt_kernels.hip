@@ -899,9 +899,10 @@ struct Variant {
     void (*frame)(TraceParams);
     void (*chain)(TraceParams);
 };
-// occupancy experiments for the headline scene (srt_set_option "occupancy" = 1 (index 2), 3, 4;
-// built with -DRT_OCC_VARIANTS, tools/build_ablations.sh); the default instantiations use
-// 2 waves/SIMD, the fastest measured (profiles/)
+// occupancy experiments for the headline scene (srt_set_option "occupancy" = 2 (1 wave/SIMD), 3, 4;
+// built with -DRT_OCC_VARIANTS); the default instantiations use RT_OCC = 3 waves/SIMD.  Same-box A/B
+// against 2 waves/SIMD (profiles/r03_occ_ab.txt): device-resident ex1 1080p 1.22 -> 1.10 ms, ex3
+// k_frame 3.36 -> 3.06 ms, ex4 4K 14.5 -> 13.2 ms, cornell 4.87 -> 4.05 s, mesh 12.2 -> 10.2 ms.
 #ifdef RT_OCC_VARIANTS
 const Variant OCC_VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>, k_frame<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1, true>},
@@ -910,15 +911,19 @@ const Variant OCC_VARIANTS[] = {
 };
 #endif
 int g_occupancy = 0;
+#ifndef RT_OCC
+#define RT_OCC 3
+#endif
+constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (register cap 512 / OCC)
 const Variant VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY>, k_frame<MATS_GLOSSY_SKY>, k_trace<MATS_GLOSSY_SKY, 2, true>},
-    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC>, k_frame<MATS_DIELECTRIC>, k_trace<MATS_DIELECTRIC, 2, true>},
-    {MATS_FILM, k_primary<MATS_FILM>, k_trace<MATS_FILM>, k_frame<MATS_FILM>, k_trace<MATS_FILM, 2, true>},
-    {MATS_MC, k_primary<MATS_MC>, k_trace<MATS_MC>, k_frame<MATS_MC>, k_trace<MATS_MC, 2, true>},
-    {MAT_ALL, k_primary<MAT_ALL>, k_trace<MAT_ALL>, k_frame<MAT_ALL>, k_trace<MAT_ALL, 2, true>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>},
+    {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
+    {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
+    {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
+    {MAT_ALL, k_primary<MAT_ALL, OCC>, k_trace<MAT_ALL, OCC>, k_frame<MAT_ALL, OCC>, k_trace<MAT_ALL, OCC, true>},
     // scenes with a triangle BVH (TriangleMesh)
-    {MAT_ALL | MAT_BVH, k_primary<MAT_ALL | MAT_BVH>, k_trace<MAT_ALL | MAT_BVH>, k_frame<MAT_ALL | MAT_BVH>,
-     k_trace<MAT_ALL | MAT_BVH, 2, true>},
+    {MAT_ALL | MAT_BVH, k_primary<MAT_ALL | MAT_BVH, OCC>, k_trace<MAT_ALL | MAT_BVH, OCC>, k_frame<MAT_ALL | MAT_BVH, OCC>,
+     k_trace<MAT_ALL | MAT_BVH, OCC, true>},
 };
 const Variant& pick_variant(uint32_t mats) {
 #ifdef RT_OCC_VARIANTS
@@ -1249,6 +1254,7 @@ struct FrameSlot {
 struct srt_ctx {
     int device = 0;
     int max_blocks = 2048;
+    int ncu = 256;
     int64_t queue_budget = (int64_t)96 << 30;  // bytes for both ray queues
     // scene
     bool has_scene = false;
@@ -1387,8 +1393,7 @@ int ensure_ring(srt_ctx* c, int64_t cap) {
     int64_t k = 256;
     while (k < cap) k <<= 1;
     cap = k;
-    int dev_cus = c->max_blocks / 8;
-    const int nslot = std::max(1024, 2 * 32 * dev_cus);
+    const int nslot = std::max(1024, 2 * 32 * c->ncu);
     if (cap <= c->f->ring_cap && nslot <= c->f->nslot) return SRT_OK;
     free_list(c->f->ring_bufs);
     c->f->ring_cap = 0;
@@ -2001,7 +2006,11 @@ int srt_create(int device, srt_ctx** out) {
     c->device = device;
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
-    c->max_blocks = prop.multiProcessorCount * 8;
+    c->ncu = prop.multiProcessorCount;
+    // 4 x OCC blocks per CU = the CU's resident wave slots (OCC per SIMD): one wave-sized block
+    // (the frame kernel) per slot, or four rounds of the OCC resident 256-thread blocks of the
+    // grid-stride kernels
+    c->max_blocks = prop.multiProcessorCount * 4 * OCC;
     int rc = ensure_slot(c->slots[0]);
     if (rc) {
         delete c;
@@ -2311,7 +2320,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         // a frame kernel block traces one 64-pixel tile through the pass's samples: a small frame (a
         // shard of a multi-GPU frame) has too few tiles to fill the GPU, so its samples are split
         // into groups, one block per (tile, group), until there are ~4 blocks per resident wave
-        // slot (c->max_blocks = 8 per CU at 2 waves/SIMD)
+        // slot (c->max_blocks = 4 OCC per CU)
         const int64_t want = 4 * (int64_t)c->max_blocks;
         const int64_t g = c->frame_groups > 0 ? c->frame_groups : (want + ntiles - 1) / ntiles;
         F.groups = (int)std::max<int64_t>(1, std::min<int64_t>(g, batch));

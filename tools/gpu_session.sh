@@ -31,6 +31,20 @@ for step in "$@"; do
     pmc_list) run pmc_list 120 rocprofv3 -L ;;
     pmc_sq) run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_sq1 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
             run pmc_sq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o bench --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc4) C=${CONFIG:-example1_1080p_d5}; T=${PMC_TAG:-r03}
+          for pass in "A:SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE" \
+                      "B:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+                      "F:FETCH_SIZE" "W:WRITE_SIZE"; do
+            k=${pass%%:*}; ctr=${pass#*:}
+            run pmc${k}_$C 240 rocprofv3 --pmc $ctr --kernel-trace -d gpurun_out/pmc_${T}_${C}_$k -o bench --output-format csv -- python3 bench.py --config $C --steps ${PMC_STEPS:-3} --warmup 1 --no-cpu-baseline --no-secondary
+          done ;;
+    shardall) for C in ${SHARD_CONFIGS:-example1_1080p_d5 example4_4k_d6 cornell_800_s512}; do
+                case $C in cornell*) st=2;; example4*) st=10;; *) st=100;; esac
+                run "whole_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup 2
+                for n in ${SHARD_NS:-2 4 8}; do
+                  run "shard${n}_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup 2 --shard-of $n --shard-rank all
+                done
+              done ;;
     mttests) run mttests 600 python3 -u -m pytest tests/test_multirank.py tests/test_mt.py tests/test_gpu.py -x -v -m gpu -k "band or shard or mt or numpy_stream or async" --timeout 300 --timeout-method thread -rf ;;
     mctests) run mctests 600 python3 -u -m pytest tests/test_gpu_mc.py -x -v -m gpu --timeout 300 --timeout-method thread -rf ;;
     shardtests) run shardtests 600 python3 -u -m pytest tests/test_gpu_shards.py -x -v -s -m gpu --timeout 300 --timeout-method thread -rf ;;
