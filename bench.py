@@ -366,7 +366,7 @@ def main():
                     help="with --shard-of: the rank rehearsed, or 'all' (every rank in turn; ms_per_step = the "
                          "slowest rank, value = all ranks' rays / that time)")
     ap.add_argument("--shard-bands", type=int, default=0,
-                    help="most row bands per rank (library option shard_bands; default rt_device.h SHARD_BANDS)")
+                    help="most row bands per rank (library option shard_bands; default rt_device.h shard_kmax)")
     ap.add_argument("--shard-snake", type=int, default=-1,
                     help="band dealing order, 0 round-robin / 1 snake (library option shard_snake; default SHARD_SNAKE)")
     args = ap.parse_args()
@@ -423,9 +423,10 @@ def main():
     npix_full = W * H
     flags = N.RENDER_SHARDED | N.RENDER_RGB_ROWS if world > 1 else 0
     rows32 = None
-    from sightpy._shard import SHARD_BANDS, SHARD_SNAKE, band_height, shard_rows
+    from sightpy._shard import SHARD_SNAKE, band_height, scene_fanout, shard_kmax, shard_rows
 
-    kmax = args.shard_bands or SHARD_BANDS
+    # the library's band count (rt_device.h shard_kmax: depends on the scene's fan-out)
+    kmax = shard_kmax(H, max(world, args.shard_of, 1), args.shard_bands, scene_fanout(sc))
     snake = args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE
     rehearse = {None: None}  # rank -> its rows (None: the frame as the launcher splits it)
     if args.shard_of > 1 and world == 1:

@@ -32,9 +32,13 @@
 #include <hip/hip_runtime.h>
 #define RT_HD __host__ __device__ __forceinline__
 #define RT_HDM __host__ __device__ __forceinline__
+// out of line on the device: code on rare paths that would otherwise be inlined at every call site
+// (instruction-cache footprint of the trace kernels) and hold registers in every kernel that calls it
+#define RT_OOL __host__ __device__ __attribute__((noinline))
 #else
 #define RT_HD static inline
 #define RT_HDM inline
+#define RT_OOL static inline
 #endif
 
 // Diagnostic build only (-DRT_PROF): wave-time per code section, sampled on 1/16 of the blocks,
@@ -152,11 +156,14 @@ RT_HD int64_t np_trunc(double x) {
 }
 // Python/numpy integer floor-mod (result has the sign of m); 64-bit division is emulated on the
 // GPU, so in-range and 32-bit operands take cheaper paths with identical results
+RT_OOL int64_t py_mod_wide(int64_t a, int64_t m) {  // emulated 64-bit division: ~150 instructions
+    int64_t r = a % m;
+    return (r != 0 && (r < 0) != (m < 0)) ? r + m : r;
+}
 RT_HD int64_t py_mod(int64_t a, int64_t m) {
     if (a >= 0 && a < m) return a;
     if (a >= 0 && a <= 0x7FFFFFFFLL && m > 0 && m <= 0x7FFFFFFFLL) return (int64_t)((uint32_t)a % (uint32_t)m);
-    int64_t r = a % m;
-    return (r != 0 && (r < 0) != (m < 0)) ? r + m : r;
+    return py_mod_wide(a, m);
 }
 
 // ---- complex128 (numpy semantics) ---------------------------------------------------------
@@ -346,19 +353,13 @@ RT_HD double collider_hit(const RT_RO srt_collider& c, d3 O, d3 D, double& o) {
     }
 }
 
-// Large libm routines called only on rare paths (the Glossy lobe's non-integer power, sphere uv)
-// are kept out of line: inlined, their temporaries set the register allocation of every shading
-// kernel (k_primary<33> at 3 waves/SIMD: 127 VGPRs spilled inlined, none out of line); the call
-// returns the same value as the inlined routine
-#ifdef __HIP_DEVICE_COMPILE__
-__device__ __attribute__((noinline)) double pow_ool(double x, double y) { return pow(x, y); }
-__device__ __attribute__((noinline)) double atan2_ool(double y, double x) { return atan2(y, x); }
-__device__ __attribute__((noinline)) double asin_ool(double x) { return asin(x); }
-#else
-inline double pow_ool(double x, double y) { return pow(x, y); }
-inline double atan2_ool(double y, double x) { return atan2(y, x); }
-inline double asin_ool(double x) { return asin(x); }
-#endif
+// Large libm routines called only on rare paths (the Glossy lobe's non-integer power, sphere uv, the
+// resolve's sRGB power) are kept out of line: inlined, their temporaries set the register
+// allocation of every shading kernel (k_primary<33> at 3 waves/SIMD: 127 VGPRs spilled inlined,
+// none out of line); the call returns the same value as the inlined routine
+RT_OOL double pow_ool(double x, double y) { return pow(x, y); }
+RT_OOL double atan2_ool(double y, double x) { return atan2(y, x); }
+RT_OOL double asin_ool(double x) { return asin(x); }
 
 // ---- normals and uv (per collider) ---------------------------------------------------------
 // cuboid.py:142-151: face normal picked by the largest scaled |local coordinate|
@@ -1118,8 +1119,20 @@ RT_HD uint32_t child_path(uint32_t path, uint32_t slot, uint32_t round) { return
 // is a run of the numpy stream a rank jumps to (~110 us of a CU per jump), so the bands are as tall
 // as the balance allows: h is chosen per (H, n) with at most `kmax` bands per rank (and at least
 // kmax / 2), the fewest rows on the busiest rank first, then the most bands.
-constexpr int SHARD_BANDS = 8;  // kmax: most bands per rank (option "shard_bands")
+constexpr int SHARD_BANDS = 8;  // kmax: most bands per rank (option "shard_bands"; 0 = shard_kmax's choice)
 constexpr int SHARD_SNAKE = 1;  // dealing order (option "shard_snake")
+// A Diffuse fan-out scene costs ~50 rays per pixel and sample, so a jump is a fraction of one row's
+// work and the balance wins: bands of SHARD_FANOUT_ROWS rows (cornell 800x800 on 8 ranks, slowest
+// rank of the same frame: 618 ms with 20-row bands, 583 with 4, 570 with 2; profiles/r03_*)
+constexpr int SHARD_FANOUT_ROWS = 2;
+RT_HD int shard_kmax(int64_t H, int n, int kmax_opt, int fanout) {
+    if (kmax_opt > 0) return kmax_opt;
+    if (fanout > 2 && n > 0) {
+        const int64_t k = H / ((int64_t)n * SHARD_FANOUT_ROWS);
+        return k > SHARD_BANDS ? (int)k : SHARD_BANDS;
+    }
+    return SHARD_BANDS;
+}
 RT_HD int shard_band_owner(int64_t b, int n, int snake) {
     const int i = (int)(b % n);
     return (snake && ((b / n) & 1)) ? n - 1 - i : i;
@@ -1158,7 +1171,7 @@ RT_HD int64_t shard_local_row(int64_t y, int n, int64_t h) { return (y / (h * n)
 RT_HD void resolve_pixel(double r, double g, double b, double& orr, double& og, double& ob, uint8_t px[3]) {
     double c[3] = {r, g, b}, e[3];
     for (int k = 0; k < 3; ++k)
-        e[k] = (c[k] <= 0.00304) ? 12.92 * c[k] : 1.055 * pow(c[k], 1.0 / 2.4) - 0.055;
+        e[k] = (c[k] <= 0.00304) ? 12.92 * c[k] : 1.055 * pow_ool(c[k], 1.0 / 2.4) - 0.055;
     double peak = np_max(np_max(e[0], e[1]), e[2]) + 0.00001;
     if (peak > 1.0)
         for (int k = 0; k < 3; ++k) e[k] = (e[k] * 1.0) / peak;

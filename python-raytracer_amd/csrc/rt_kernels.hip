@@ -1348,7 +1348,7 @@ struct srt_ctx {
     int nranks = 1, rank = 0;
     bool defer_gather = false;  // srt_render_group posts the gathers of all its contexts in one group
     bool retry_frame = false;   // the last finish_async failed only with RETRY_* bits (render the frame again)
-    int shard_bands = SHARD_BANDS;  // option "shard_bands": most row bands per rank (rt_device.h shard_band_height)
+    int shard_bands = 0;  // option "shard_bands": most row bands per rank (0: rt_device.h shard_kmax by the scene's fan-out)
     int shard_snake = SHARD_SNAKE;  // option "shard_snake": bands dealt in alternating direction per period
     int frame_groups = 0;           // option "frame_groups": k_frame sample groups per tile (0: auto)
     double* red = nullptr;      // srt_comm_allreduce scratch
@@ -2059,7 +2059,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         return SRT_OK;
     }
     if (!strcmp(key, "shard_bands")) {
-        if (value < 1 || value > 4096) return fail(SRT_ERR_ARG, "shard_bands: 1..4096");
+        if (value < 0 || value > 4096) return fail(SRT_ERR_ARG, "shard_bands: 0 (auto) .. 4096");
         c->shard_bands = (int)value;
         return SRT_OK;
     }
@@ -2259,7 +2259,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (c->nranks > MAX_RANKS) return fail(SRT_ERR_ARG, "too many ranks");
         if (cam->height < c->nranks) return fail(SRT_ERR_ARG, "a sharded frame needs at least one row per rank");
         if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
-        band = shard_band_height(cam->height, c->nranks, c->shard_bands, c->shard_snake);
+        band = shard_band_height(cam->height, c->nranks, shard_kmax(cam->height, c->nranks, c->shard_bands, c->fanout),
+                                 c->shard_snake);
         rows_h = band_rows(cam->height, c->nranks, c->rank, band, c->shard_snake);
         n_rows = (int)rows_h.size();
         rows_src = rows_h.data();

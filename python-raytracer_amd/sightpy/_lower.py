@@ -167,12 +167,41 @@ _GREY_CACHE = collections.OrderedDict()  # id(grey image) -> (image, RGB copy, f
 _GREY_CACHE_MAX = 16
 
 
+_FP_CACHE = collections.OrderedDict()  # (id(root), address, shape, strides) -> (root, fingerprint), LRU
+_FP_CACHE_MAX = 64
+
+
+def _immutable_root(a):
+    """The `bytes` object holding `a`'s texels when nothing can write them (images decoded by PIL:
+    np.asarray(img) is a read-only view of immutable bytes), else None."""
+    b = a
+    while isinstance(b, np.ndarray):
+        if b.flags.writeable:
+            return None
+        if b.base is None:
+            return None
+        b = b.base
+    return b if isinstance(b, bytes) else None
+
+
 def _fingerprint(a):
-    """Content hash of a texture (xxh3: ~2 ms for the 37.7 MB stormydays image)."""
+    """Content hash of a texture (xxh3: ~2 ms for the 37.7 MB stormydays image on every Scene.render).
+    Texels that no one can modify (a read-only view of immutable bytes) are hashed once: the hash is
+    cached by their memory, and the cache holds the bytes so the key stays unique."""
+    root = _immutable_root(a) if isinstance(a, np.ndarray) else None
+    if root is not None:
+        key = (id(root), a.__array_interface__["data"][0], a.shape, a.strides)
+        hit = _FP_CACHE.get(key)
+        if hit is not None and hit[0] is root:
+            _FP_CACHE.move_to_end(key)
+            return hit[1]
     buf = memoryview(np.ascontiguousarray(a)).cast("B")
-    if _xxhash is not None:
-        return _xxhash.xxh3_64_intdigest(buf)
-    return zlib.crc32(buf)
+    fp = _xxhash.xxh3_64_intdigest(buf) if _xxhash is not None else zlib.crc32(buf)
+    if root is not None:
+        _FP_CACHE[key] = (root, fp)
+        while len(_FP_CACHE) > _FP_CACHE_MAX:
+            _FP_CACHE.popitem(last=False)
+    return fp
 
 
 def _medium_f0(n_ray, n_mat):

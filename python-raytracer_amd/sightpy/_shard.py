@@ -13,12 +13,40 @@ rank 0 over RCCL and assembles the frame there.  The image is independent of the
 
 Every band of a rank is a run of numpy's stream that the rank's generator jumps to (one ~110 us jump
 per band, plane and sample), so h is as large as the balance allows: at most `kmax` bands per rank
-(at least kmax // 2), the fewest rows on the busiest rank first, then the most bands.
+(at least kmax // 2), the fewest rows on the busiest rank first, then the most bands; a Diffuse
+fan-out scene, whose rows cost ~30x more, takes 2-row bands (shard_kmax).
 """
 import numpy as np
 
-SHARD_BANDS = 8  # kmax (library option "shard_bands")
+SHARD_BANDS = 8  # kmax (library option "shard_bands"; 0 = shard_kmax's choice)
 SHARD_SNAKE = 1  # dealing order (library option "shard_snake")
+SHARD_FANOUT_ROWS = 2  # band rows of a Diffuse fan-out scene (rt_device.h shard_kmax)
+
+
+def shard_kmax(height, world, kmax=0, fanout=1):
+    """Most bands per rank (rt_device.h shard_kmax): `kmax` if set, else SHARD_BANDS, or for a scene
+    with a Diffuse fan-out (fanout > 2: ~50 rays per pixel and sample, a jump is a fraction of one
+    row's work) as many as SHARD_FANOUT_ROWS-row bands give."""
+    if kmax:
+        return int(kmax)
+    if fanout > 2 and world > 0:
+        return max(SHARD_BANDS, int(height) // (int(world) * SHARD_FANOUT_ROWS))
+    return SHARD_BANDS
+
+
+def scene_fanout(scene):
+    """Most children one hit spawns (the library's rule, srt_upload_scene): 2 for refraction and thin
+    film, diffuse_rays for Diffuse, else 1."""
+    from . import _native as N
+    from ._lower import lower_scene
+
+    fan = 1
+    for m in lower_scene(scene).materials:
+        if m["type"] in (N.REFRACTIVE, N.THINFILM):
+            fan = max(fan, 2)
+        elif m["type"] == N.DIFFUSE:
+            fan = max(fan, max(1, int(m["ival"])))
+    return fan
 
 
 def band_owner(b, world, snake=SHARD_SNAKE):
@@ -36,12 +64,12 @@ def rank_rows(height, world, rank, band, snake=SHARD_SNAKE):
     return nb * band - ((B * band - height) if owners[-1] == rank else 0)
 
 
-def band_height(height, world, kmax=SHARD_BANDS, snake=SHARD_SNAKE):
+def band_height(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
     """Band height of a `world`-rank frame of `height` rows (rt_device.h shard_band_height)."""
     height = int(height)
     if world <= 1 or height <= 1:
         return max(height, 1)
-    kmax = max(int(kmax), 1)
+    kmax = max(shard_kmax(height, world, kmax, fanout), 1)
     best_h, best_rows = 1, None
     for k in range(kmax, max(kmax // 2, 1) - 1, -1):
         h = max(-(-height // (world * k)), 1)
@@ -51,24 +79,24 @@ def band_height(height, world, kmax=SHARD_BANDS, snake=SHARD_SNAKE):
     return best_h
 
 
-def shard_rows(height, world, rank, kmax=SHARD_BANDS, snake=SHARD_SNAKE):
+def shard_rows(height, world, rank, kmax=0, snake=SHARD_SNAKE, fanout=1):
     """Image rows owned by `rank` (ascending)."""
-    h = band_height(height, world, kmax, snake)
+    h = band_height(height, world, kmax, snake, fanout)
     rows = np.arange(int(height))
     return rows[band_owner(rows // h, world, snake) == rank]
 
 
-def max_shard_rows(height, world, kmax=SHARD_BANDS, snake=SHARD_SNAKE):
+def max_shard_rows(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
     """Largest per-rank row count (the padded tile height of the gather)."""
-    return max(len(shard_rows(height, world, r, kmax, snake)) for r in range(world))
+    return max(len(shard_rows(height, world, r, kmax, snake, fanout)) for r in range(world))
 
 
-def assemble_index(height, world, kmax=SHARD_BANDS, snake=SHARD_SNAKE):
+def assemble_index(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
     """For every image row, its position in the gathered buffer of padded tiles:
     `gathered.reshape(world * maxrows, ...)[idx]` is the image."""
-    maxrows = max_shard_rows(height, world, kmax, snake)
+    maxrows = max_shard_rows(height, world, kmax, snake, fanout)
     idx = np.empty(int(height), dtype=np.int64)
     for r in range(world):
-        rows = shard_rows(height, world, r, kmax, snake)
+        rows = shard_rows(height, world, r, kmax, snake, fanout)
         idx[rows] = r * maxrows + np.arange(len(rows))
     return idx

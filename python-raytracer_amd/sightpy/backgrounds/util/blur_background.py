@@ -45,7 +45,8 @@ def blur_skybox_u8(cross_u8, blur, cubemap=""):
         img = Image.fromarray(canvas, "RGB").filter(ImageFilter.GaussianBlur(radius=blur))
         r, c = _CROSS[name]
         out[r * n:(r + 1) * n, c * n:(c + 1) * n] = np.asarray(img)[n:2 * n, n:2 * n]
-    return out
+    # immutable texels, like an image decoded by PIL: the scene lowering hashes them only once
+    return np.frombuffer(out.tobytes(), dtype=np.uint8).reshape(out.shape)
 
 
 def blur_skybox(img_array, blur, cubemap):

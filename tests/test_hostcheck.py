@@ -52,6 +52,36 @@ def test_texel_pool_persists_across_lowerings():
     assert c.texel_key != a.texel_key and c.texels.size != a.texels.size
 
 
+def test_fingerprint_cached_only_for_immutable_texels(monkeypatch):
+    """Scene.render re-lowers its scene every call: decoded images (read-only views of immutable
+    bytes, also the blurred skybox) are hashed once; a writeable texel array is hashed on every
+    lowering, so an in-place edit still changes the key."""
+    from sightpy import _lower
+
+    calls = []
+    real = _lower._xxhash.xxh3_64_intdigest
+
+    def counting(buf):
+        calls.append(len(buf))
+        return real(buf)
+
+    monkeypatch.setattr(_lower._xxhash, "xxh3_64_intdigest", counting)
+    frozen = np.frombuffer(bytes(range(256)) * 3, dtype=np.uint8).reshape(16, 16, 3)
+    assert _lower._immutable_root(frozen) is not None
+    k1 = _lower._fingerprint(frozen)
+    assert _lower._fingerprint(frozen) == k1 and len(calls) == 1
+    live = np.array(frozen)
+    assert _lower._immutable_root(live) is None
+    assert _lower._fingerprint(live) == k1 and len(calls) == 2
+    live[0, 0, 0] ^= 1
+    assert _lower._fingerprint(live) != k1 and len(calls) == 3
+    sc = scenes.example4(16, 12, 2)
+    _lower.lower_scene(sc)
+    n = len(calls)
+    _lower.lower_scene(sc)
+    assert len(calls) == n, "a second lowering of the same scene re-hashed its textures"
+
+
 def test_glossy_integer_lobe_exponent():
     """Glossy lobe exponent a = 2/roughness^2 - 2 (glossy.py:71): lowered with an integer k in
     `ival` only when a is within 4 ulp of k (roughness 0.2 -> 47.99999999999999 -> 48, 0.5 -> 6),

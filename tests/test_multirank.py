@@ -93,6 +93,35 @@ def test_kernel_shard_map_matches_partition(H, n, kmax, snake):
         assert np.array_equal(rows // (h * n), np.arange(len(rows)) // h)
 
 
+@pytest.mark.parametrize("H,n", [(800, 8), (800, 2), (1080, 8), (2160, 8), (37, 3), (8, 8)])
+@pytest.mark.parametrize("kmax,fanout", [(0, 1), (0, 2), (0, 20), (5, 20), (0, 3)])
+def test_kernel_band_count_rule_matches_partition(H, n, kmax, fanout):
+    """The library's automatic band count (rt_device.h shard_kmax: 8 bands per rank, or 2-row bands
+    for a Diffuse fan-out scene) is the one sightpy._shard restates."""
+    import hostcheck as HC
+    from sightpy._shard import shard_kmax, band_height
+
+    lib = HC.lib()
+    lib.hc_shard_kmax.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.hc_shard_kmax.restype = ctypes.c_int
+    k = lib.hc_shard_kmax(H, n, kmax, fanout)
+    assert k == shard_kmax(H, n, kmax, fanout)
+    owner, local, h = _kernel_shard_map(H, n, k, 1)
+    assert h == band_height(H, n, kmax, 1, fanout)
+    if fanout > 2 and not kmax and H >= 4 * n * 8:
+        assert h <= 4  # k in [kmax / 2, kmax]: at most twice the 2-row bands
+
+
+def test_cornell_scene_takes_two_row_bands():
+    import scenes
+    from sightpy._shard import scene_fanout, band_height
+
+    assert scene_fanout(scenes.cornell(40, 40)) == 20
+    assert scene_fanout(scenes.example1(16, 12)) == 1
+    assert scene_fanout(scenes.example4(16, 12, 2)) == 2
+    assert band_height(800, 8, fanout=20) == 2 and band_height(1080, 8, fanout=1) == 27
+
+
 def _gather_worker(rank, world, port, H, W):
     for p in (ROOT / "python-raytracer_amd", ROOT / "tests", ROOT / "oracle"):
         sys.path.insert(0, str(p))
@@ -306,7 +335,7 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax, snake):
         assert np.array_equal(frame.reshape(3, -1), full.rgb)
     finally:
         lib.srt_set_option(ctx, b"rehearse_shard", 0)
-        lib.srt_set_option(ctx, b"shard_bands", SHARD_BANDS)
+        lib.srt_set_option(ctx, b"shard_bands", 0)  # back to the automatic choice
         lib.srt_set_option(ctx, b"shard_snake", SHARD_SNAKE)
         lib.srt_host_free(ctx, host)
 
