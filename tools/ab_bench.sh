@@ -15,7 +15,7 @@ line = [x for x in open("gpurun_out/ab_run.log") if x.startswith("{")][-1]
 d = json.loads(line)
 print(sys.argv[1].split("/")[-1], " ".join(sys.argv[2:]), "frame_ms", d["ms_per_step"],
       "resident_ms", d.get("device_resident", {}).get("ms_per_step"),
-      "kernel_ms", d.get("roofline", {}).get("kernel_ms"), flush=True)
+      "kernel_ms", d.get("roofline", {}).get("kernel_ms"), "ranks", d.get("rank_frame_ms"), flush=True)
 EOF
   done
 done

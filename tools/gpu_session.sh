@@ -54,7 +54,7 @@ for step in "$@"; do
     mt) run mt 300 python3 tools/mt_timing.py ;;
     api) run api 300 python3 tools/api_timing.py --repeats 5 --profile ;;
     api_prof) run api_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/api_prof -o api --output-format csv -- python3 tools/api_timing.py --repeats 5 ;;
-    shardprof) run shardprof_${SHARD:-8} 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/shardprof_${SHARD:-8} -o s --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-secondary --shard-of ${SHARD:-8} ;;
+    shardprof) run shardprof_${SHARD:-8}_r${SHARD_RANK:-0} 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/shardprof_${SHARD:-8}_r${SHARD_RANK:-0} -o s --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 20 --warmup 2 --no-cpu-baseline --no-secondary --shard-of ${SHARD:-8} --shard-rank ${SHARD_RANK:-0} ;;
     profsync) run profsync 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsync -o bench --output-format csv -- python3 bench.py --sync --no-cpu-baseline --no-secondary ;;
     rngdev) run bench_rngdev 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --rng device ;;
     *) echo "unknown step $step"; exit 2 ;;
