@@ -265,7 +265,8 @@ typedef struct srt_stats {
     double ms_primary_kernel;
     int64_t retries;         /* passes re-run after a queue overflow */
     int32_t kernel_path;     /* 0: per-depth wavefront kernels (ms_primary_kernel = k_primary),
-                                1: frame kernel (ms_primary_kernel = k_frame, the whole pass) */
+                                1: frame kernel (ms_primary_kernel = k_frame, the whole pass),
+                                2: fused paths (k_primary traces every depth; option fuse_primary) */
     int32_t chain_from;      /* > 0: depths >= chain_from traced in chain mode by one k_trace */
 } srt_stats;
 

@@ -438,84 +438,6 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     RT_ACC(2, tw0);
 }
 
-// Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
-// (camera.py:51-85) and tracing it; the pixel's depth-0 colour is summed in registers and added to
-// the framebuffer once (no other thread touches the pixel during this launch).
-// Copy the first `nlut` texture lookup tables into LDS (dynamic shared memory) and point the
-// scene view at them: texel -> value becomes an LDS read instead of a dependent global load.
-__device__ __forceinline__ void stage_luts(TraceParams& P) {
-    extern __shared__ double lds_lut[];
-    const int n = P.S.nlut_lds;
-    for (int i = threadIdx.x; i < n * 256; i += BLOCK) lds_lut[i] = P.S.tex[i >> 8].lut[i & 255];
-    P.S.lut_lds = (const RT_LDS double*)lds_lut;
-    __syncthreads();
-}
-
-template <uint32_t MATS, int OCC = 2>
-__global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
-    TraceParams P = P0;
-    stage_luts(P);
-    const uint32_t shard = blockIdx.x % NSHARD;
-    uint32_t err = 0;
-    uint32_t shadow = 0;
-    const int64_t ngroups = (P.spp + P.spt - 1) / P.spt;
-    const int64_t n = P.npix * ngroups;
-    const Quot qw((double)P.cam.width), qh((double)P.cam.height);
-    for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
-        const int64_t i = base + threadIdx.x;
-        const bool active = i < n;
-        const int64_t grp = active ? i / P.npix : 0;
-        const uint32_t p = active ? (uint32_t)(i - grp * P.npix) : 0u;
-        const int s_begin = (int)grp * P.spt, s_end = min(P.spp, s_begin + P.spt);
-        const uint32_t lr = p / (uint32_t)P.cam.width;
-        const uint32_t col = p - lr * (uint32_t)P.cam.width;
-        const int grow = active ? P.rows[lr] : 0;
-        const double xc = active ? P.cam.xs[col] : 0.0, yr = active ? P.cam.ys[grow] : 0.0;
-        d3 acc = d3{0.0, 0.0, 0.0};
-        const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
-        // software pipeline: the next sample's uniforms are loaded while this sample is traced
-        double jn[4] = {0.0, 0.0, 0.0, 0.0};
-        if (active) primary_uniforms(P, s_begin, p, gpix, jn);
-        for (int s = s_begin; s < s_end; ++s) {
-            Ray r;
-            r.o = r.d = d3{0.0, 0.0, 0.0};
-            r.w = d3{1.0, 1.0, 1.0};
-            r.meta = pack_meta(0, 0, 0);
-            r.pix = p;
-            r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
-            const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
-            RT_T0(tr0);
-            if (active && s + 1 < s_end) primary_uniforms(P, s + 1, p, gpix, jn);
-            if (active) primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
-            RT_ACC(0, tr0);
-            int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
-            RT_T0(tt0);
-            trace_one<MATS>(P, r, active, err, hs, GpuEmit{P, r, shard, 0u, &shadow, &acc});
-            RT_ACC(3, tt0);
-        }
-        if (ngroups > 1) {
-            if (active) fb_add(P.fb, P.fbx, P.flags, P.npix, p, d3{1.0, 1.0, 1.0}, acc);
-        } else if (active && P.fb_first) {
-            P.fb[p] = acc.x;
-            P.fb[P.npix + p] = acc.y;
-            P.fb[2 * P.npix + p] = acc.z;
-            if (P.fbx) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = 0ull;  // this frame's fixed-point sums start here
-                fx_mag(P.fbx, P.npix)[p] = 0.0f;
-            }
-        } else if (active && !is_zero(acc)) {
-            P.fb[p] += acc.x;
-            P.fb[P.npix + p] += acc.y;
-            P.fb[2 * P.npix + p] += acc.z;
-        }
-    }
-    if (err) atomicOr(&P.flags[0], err);
-    if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
-}
-
-// Depth d >= 1: blocks b, b + NSHARD, ... drain input shard b % NSHARD and append to output shard
-// b % NSHARD.
 // Chain mode emitter (scenes whose rays have at most one child): the child replaces the ray in the
 // thread instead of going to the next depth's queue.  A second child (two colliders tied at the
 // same distance) has no place: it raises the retry flag and the host renders the frame again
@@ -555,6 +477,129 @@ struct ChainEmit {
     }
 };
 
+// Fused-path emitter (k_primary<.., FUSE>: single-child scenes traced pixel by pixel, every depth
+// in the pixel's own thread): colour of every depth into the thread's register sum, the one child
+// replaces the ray.  A second child (an exact tie) raises RETRY_CHAIN_TIE as in chain mode.
+struct FusedEmit {
+    const TraceParams& P;
+    const Ray& r;
+    uint32_t round;
+    uint32_t* shadow_acc;
+    d3* acc;
+    Ray* next;
+    bool* has;
+
+    __device__ void local(d3 c) const {
+        if (!is_zero(c)) *acc = add(*acc, mul(r.w, c));
+    }
+    __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
+    __device__ void child(const Child& c) const {
+        ChainEmit{P, r, round, shadow_acc, next, has}.child(c);
+    }
+    __device__ void diffuse(const DiffuseGen& g, int mi) const {
+        ChainEmit{P, r, round, shadow_acc, next, has}.diffuse(g, mi);
+    }
+};
+
+// Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
+// (camera.py:51-85) and tracing it; the pixel's depth-0 colour is summed in registers and added to
+// the framebuffer once (no other thread touches the pixel during this launch).
+// Copy the first `nlut` texture lookup tables into LDS (dynamic shared memory) and point the
+// scene view at them: texel -> value becomes an LDS read instead of a dependent global load.
+__device__ __forceinline__ void stage_luts(TraceParams& P) {
+    extern __shared__ double lds_lut[];
+    const int n = P.S.nlut_lds;
+    for (int i = threadIdx.x; i < n * 256; i += BLOCK) lds_lut[i] = P.S.tex[i >> 8].lut[i & 255];
+    P.S.lut_lds = (const RT_LDS double*)lds_lut;
+    __syncthreads();
+}
+
+template <uint32_t MATS, int OCC = 2, bool FUSE = false>
+__global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
+    TraceParams P = P0;
+    stage_luts(P);
+    const uint32_t shard = blockIdx.x % NSHARD;
+    uint32_t err = 0;
+    uint32_t shadow = 0;
+    const int64_t ngroups = (P.spp + P.spt - 1) / P.spt;
+    const int64_t n = P.npix * ngroups;
+    const Quot qw((double)P.cam.width), qh((double)P.cam.height);
+    for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const bool active = i < n;
+        const int64_t grp = active ? i / P.npix : 0;
+        const uint32_t p = active ? (uint32_t)(i - grp * P.npix) : 0u;
+        const int s_begin = (int)grp * P.spt, s_end = min(P.spp, s_begin + P.spt);
+        const uint32_t lr = p / (uint32_t)P.cam.width;
+        const uint32_t col = p - lr * (uint32_t)P.cam.width;
+        const int grow = active ? P.rows[lr] : 0;
+        const double xc = active ? P.cam.xs[col] : 0.0, yr = active ? P.cam.ys[grow] : 0.0;
+        d3 acc = d3{0.0, 0.0, 0.0};
+        const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
+        // software pipeline: the next sample's uniforms are loaded while this sample is traced
+        double jn[4] = {0.0, 0.0, 0.0, 0.0};
+        if (active) primary_uniforms(P, s_begin, p, gpix, jn);
+        for (int s = s_begin; s < s_end; ++s) {
+            Ray r;
+            r.o = r.d = d3{0.0, 0.0, 0.0};
+            r.w = d3{1.0, 1.0, 1.0};
+            r.meta = pack_meta(0, 0, 0);
+            r.pix = p;
+            r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
+            const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
+            RT_T0(tr0);
+            if (active && s + 1 < s_end) primary_uniforms(P, s + 1, p, gpix, jn);
+            if (active) primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
+            RT_ACC(0, tr0);
+            int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
+            RT_T0(tt0);
+            if (!FUSE) {
+                trace_one<MATS>(P, r, active, err, hs, GpuEmit{P, r, shard, 0u, &shadow, &acc});
+            } else {
+                // the sample's whole path in this thread (single-child scenes): no queue, every
+                // depth's colour into `acc`; the lanes of an iteration share a depth, counted per
+                // wave into the shard's counter of that depth as the queue appends would have been
+                Ray nx = r;
+                bool has = false;
+                trace_one<MATS>(P, r, active, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &nx, &has});
+                bool live = active && has;
+                for (int d = 1;; ++d) {
+                    const uint64_t m = __ballot(live);
+                    if (m == 0) break;
+                    if (live && lanes_below(m) == 0 && d < SRT_MAX_DEPTHS)  // the lowest live lane
+                        atomicAdd(P.cnt_out + (int64_t)(d - 1) * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
+                    if (d > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
+                    r = nx;
+                    has = false;
+                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &nx, &has});
+                    live = live && has;
+                }
+            }
+            RT_ACC(3, tt0);
+        }
+        if (ngroups > 1) {
+            if (active) fb_add(P.fb, P.fbx, P.flags, P.npix, p, d3{1.0, 1.0, 1.0}, acc);
+        } else if (active && P.fb_first) {
+            P.fb[p] = acc.x;
+            P.fb[P.npix + p] = acc.y;
+            P.fb[2 * P.npix + p] = acc.z;
+            if (P.fbx) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = 0ull;  // this frame's fixed-point sums start here
+                fx_mag(P.fbx, P.npix)[p] = 0.0f;
+            }
+        } else if (active && !is_zero(acc)) {
+            P.fb[p] += acc.x;
+            P.fb[P.npix + p] += acc.y;
+            P.fb[2 * P.npix + p] += acc.z;
+        }
+    }
+    if (err) atomicOr(&P.flags[0], err);
+    if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+}
+
+// Depth d >= 1: blocks b, b + NSHARD, ... drain input shard b % NSHARD and append to output shard
+// b % NSHARD.
 template <uint32_t MATS, int OCC = 2, bool CHAIN = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
     TraceParams P = P0;
@@ -898,6 +943,7 @@ struct Variant {
     void (*trace)(TraceParams);
     void (*frame)(TraceParams);
     void (*chain)(TraceParams);
+    void (*fused)(TraceParams) = nullptr;  // k_primary<.., FUSE>: whole single-child paths per pixel
 };
 // occupancy experiments for the headline scene (srt_set_option "occupancy" = 2 (1 wave/SIMD), 3, 4;
 // built with -DRT_OCC_VARIANTS); the default instantiations use RT_OCC = 3 waves/SIMD.  Same-box A/B
@@ -915,8 +961,12 @@ int g_occupancy = 0;
 #define RT_OCC 3
 #endif
 constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (register cap 512 / OCC)
+#ifndef RT_FUSE_OCC
+#define RT_FUSE_OCC 2  // the fused k_primary holds the next ray as well: 45 VGPRs spilled at 3 waves/SIMD
+#endif
 const Variant VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
+     k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>},
     {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
     {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
@@ -1165,6 +1215,7 @@ __global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, cons
 struct FramePlan {
     bool frame = false;  // rendered by k_frame (counts are totals, not queue fills)
     int chain_from = 0;  // > 0: k_trace at this depth runs in chain mode and no deeper kernel is launched
+    bool fuse = false;   // k_primary traces every depth (single-child scenes): no k_trace launch
     int64_t npix = 0;
     int64_t W = 0, H = 0;  // frame shape (a shard renders npix of W * H)
     bool sharded = false, gather_rgb = false, use_mt = false;
@@ -1351,6 +1402,7 @@ struct srt_ctx {
     int shard_bands = 0;  // option "shard_bands": most row bands per rank (0: rt_device.h shard_kmax by the scene's fan-out)
     int shard_snake = SHARD_SNAKE;  // option "shard_snake": bands dealt in alternating direction per period
     int frame_groups = 0;           // option "frame_groups": k_frame sample groups per tile (0: auto)
+    int fuse_primary = 0;           // option "fuse_primary": single-child scenes traced whole-path per pixel in k_primary
     double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
@@ -1786,7 +1838,7 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S, uint32_t* retry 
     for (int d = 0; d < SRT_MAX_DEPTHS; ++d) S.rays_per_depth[d] = 0;
     for (int p = 0; p < F.npass; ++p) {
         const uint32_t* hp = c->f->host + p * F.pass_words;
-        if (depth_total(hp + (int64_t)(F.dcap + 1) * NSHARD, F.frame ? INT64_MAX : c->f->seg) != 0)
+        if (depth_total(hp + (int64_t)(F.dcap + 1) * NSHARD, (F.frame || F.fuse) ? INT64_MAX : c->f->seg) != 0)
             return fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
         if (F.frame) {
             // k_frame counts every ray it traces (per shard), depth 0 included
@@ -1794,7 +1846,8 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S, uint32_t* retry 
                 for (int k = 0; k < NSHARD; ++k) S.rays_per_depth[d] += hp[(int64_t)d * NSHARD + k];
         } else {
             S.rays_per_depth[0] += (int64_t)std::min(F.batch, F.spp - p * F.batch) * F.npix;
-            for (int d = 1; d <= F.dcap; ++d) S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, c->f->seg);
+            for (int d = 1; d <= F.dcap; ++d)
+                S.rays_per_depth[d] += depth_total(hp + (int64_t)d * NSHARD, F.fuse ? INT64_MAX : c->f->seg);
         }
         const hipEvent_t* ev = c->f->ev.data() + (int64_t)p * F.nev;
         float ms;
@@ -1810,7 +1863,7 @@ int collect_frame(srt_ctx* c, const FramePlan& F, srt_stats& S, uint32_t* retry 
     S.ms_device = ms_trace;
     S.shadow_rays = (int64_t)(hshadow[0] | (uint64_t)hshadow[1] << 32);
     S.n_depths = F.dcap + 1;
-    S.kernel_path = F.frame ? 1 : 0;
+    S.kernel_path = F.frame ? 1 : (F.fuse ? 2 : 0);
     S.chain_from = F.chain_from;
     S.total_rays = 0;
     for (int d = 0; d <= F.dcap; ++d) S.total_rays += S.rays_per_depth[d];
@@ -2064,6 +2117,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         return SRT_OK;
     }
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
+    if (!strcmp(key, "fuse_primary")) { c->fuse_primary = (int)value; return SRT_OK; }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
     if (!strcmp(key, "deterministic")) {
@@ -2326,7 +2380,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         const int64_t g = c->frame_groups > 0 ? c->frame_groups : (want + ntiles - 1) / ntiles;
         F.groups = (int)std::max<int64_t>(1, std::min<int64_t>(g, batch));
     }
-    if (!F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
+    F.fuse = !F.frame && c->fanout == 1 && c->chain_ok && c->fuse_primary > 0 && pick_variant(c->mats).fused;
+    if (!F.fuse && !F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
         c->hint_key[2] == batch) {
         for (int d = 1; d <= F.dcap; ++d)
             if (c->hint[d] < c->chain_rays) { F.chain_from = d; break; }
@@ -2377,7 +2432,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                           jit_doubles <= c->f->jit_cap && (!use_mt || mt_win_need <= c->f->mt_win_cap) &&
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
                           (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
-                          F.frame == pp.frame && F.chain_from == pp.chain_from && F.W == pp.W && F.H == pp.H &&
+                          F.frame == pp.frame && F.chain_from == pp.chain_from && F.fuse == pp.fuse && F.W == pp.W && F.H == pp.H &&
                           F.groups == pp.groups && (F.groups == 1 || (int64_t)F.groups * 3 * npix <= c->f->fbg_cap) &&
                           F.sharded == pp.sharded && F.gather_rgb == pp.gather_rgb && F.use_mt == pp.use_mt &&
                           (!sharded || c->rank != 0 ||
@@ -2630,17 +2685,20 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.n_primary = nrays;
             P.qout = c->f->q[1];
             P.cnt_out = c->f->counts + NSHARD;
+            P.dcap = F.dcap;
             HIP_TRY(hipEventRecord(ev[0], c->f->stream));
-            hipLaunchKernelGGL(V.primary, dim3(grid_for(npix * ((ns + P.spt - 1) / P.spt), c->max_blocks)),
+            hipLaunchKernelGGL(F.fuse ? V.fused : V.primary, dim3(grid_for(npix * ((ns + P.spt - 1) / P.spt), c->max_blocks)),
                                dim3(BLOCK), lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
+            if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
+                for (int d = 1; d <= F.dcap; ++d) HIP_TRY(hipEventRecord(ev[1 + d], c->f->stream));
             if (mst != c->f->stream) {  // the next generation into this slot may start
                 HIP_TRY(hipEventRecord(c->f->jit_free, c->f->stream));
                 c->f->jit_busy = true;
             }
             P.fb_first = 0;
-            for (int d = 1; d <= F.dcap; ++d) {
+            for (int d = 1; d <= F.dcap && !F.fuse; ++d) {
                 if (F.chain_from > 0 && d > F.chain_from) break;  // traced by the chain kernel
                 P.depth = d;
                 P.qin = c->f->q[d & 1];
@@ -2773,7 +2831,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             // child (the same tie would recur), with bigger queues after an overflow
             S.retries = retries + 1;
             if (S.retries > 8) return fail(SRT_ERR_MEMORY, "ray queues keep overflowing");
-            if (bits & RETRY_CHAIN_TIE) F.chain_from = 0;
+            if (bits & RETRY_CHAIN_TIE) {
+                F.chain_from = 0;
+                F.fuse = false;
+            }
             if ((bits & RETRY_OVERFLOW) &&
                 (rc = F.frame ? ensure_ring(c, 2 * c->f->ring_cap) : ensure_queues(c, 2 * c->f->seg * NSHARD)))
                 return rc;

@@ -190,7 +190,7 @@ class Stats(ctypes.Structure):
             "ms_trace_kernels": float(self.ms_trace_kernels),
             "ms_primary_kernel": float(self.ms_primary_kernel),
             "retries": int(self.retries),
-            "kernel_path": "frame" if int(self.kernel_path) == 1 else "wavefront",
+            "kernel_path": {1: "frame", 2: "fused"}.get(int(self.kernel_path), "wavefront"),
             "chain_from": int(self.chain_from),
         }
 

@@ -218,11 +218,12 @@ def _set_option(key, value):
 
 
 @pytest.mark.parametrize("name,builder,depth", DETERMINISTIC)
-@pytest.mark.parametrize("mode", ["wavefront", "wavefront+chain", "frame"])
+@pytest.mark.parametrize("mode", ["wavefront", "wavefront+chain", "frame", "fused"])
 def test_gpu_every_kernel_path_matches_reference(name, builder, depth, mode):
     """Every example through each trace strategy, whatever the automatic choice would be: the
     per-depth wavefront kernels, the same with chain mode from depth 2 (the second render of a
-    shape; single-child scenes only), and the frame kernel."""
+    shape; single-child scenes only), the frame kernel, and the fused paths (every depth of a
+    single-child scene in k_primary)."""
     g = golden(name)
     W, H, spp = int(g["width"]), int(g["height"]), int(g["spp"])
     sc = builder(W, H, depth)
@@ -230,6 +231,7 @@ def test_gpu_every_kernel_path_matches_reference(name, builder, depth, mode):
     jit = sc.camera.draw_jitter(spp)
     _set_option("frame_kernel", 1 if mode == "frame" else 0)
     _set_option("chain_rays", 1 << 40 if mode == "wavefront+chain" else 0)
+    _set_option("fuse_primary", 1 if mode == "fused" else 0)
     try:
         B = _backend()
         for _ in range(2 if mode == "wavefront+chain" else 1):
@@ -237,6 +239,9 @@ def test_gpu_every_kernel_path_matches_reference(name, builder, depth, mode):
     finally:
         _set_option("frame_kernel", -1)
         _set_option("chain_rays", 1000000)
+        _set_option("fuse_primary", 0)
+    if mode == "fused" and builder is scenes.example1:
+        assert out.stats["kernel_path"] == "fused"
     assert np.array_equal(out.hit_ids, g["hit_id"])
     assert out.stats["rays_per_depth"][: len(g["depth_counts"])] == g["depth_counts"].tolist()
     np.testing.assert_allclose(out.rgb, g["rgb"], rtol=RTOL, atol=ATOL)
