@@ -24,6 +24,9 @@ structured like the reference's Scene.render).
 import os
 
 os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # CPU baseline legs: one BLAS thread per process
+# seven hardware queues per process (HIP's default is four; read when HIP initialises, inherited by the
+# ranks): the library then keeps six frames in flight (rt_kernels.hip default_slots)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "7")
 import argparse
 import ctypes
 import json
@@ -119,7 +122,8 @@ def _pool_task(args):
 
 # CPU sample per config: the headline frames whole; the 4K and 512-spp frames on
 # one row tile (rank 0's rows of an 8-rank job), rates extrapolated to the frame
-CPU_TILE = {"example4_4k_d6": 8, "cornell_800_s512": 8, "mesh_1080p_d3": 8}
+# (the TriangleMesh frame: 4 rows of 1920 pixels, the oracle intersects all 20,480 triangles per ray)
+CPU_TILE = {"example4_4k_d6": 8, "cornell_800_s512": 8, "mesh_1080p_d3": 270}
 
 
 def cpu_baseline(builder, W, H, depth, spp, frame_rays, tile_of=0, budget_s=15.0):

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -1224,7 +1225,7 @@ struct FramePlan {
     int64_t cnt_words = 0, pass_words = 0;
 };
 
-constexpr int MAX_FRAME_SLOTS = 4;
+constexpr int MAX_FRAME_SLOTS = 8;
 
 // Buffers and stream of one frame in flight.  Synchronous calls use slot 0; pipelined
 // (SRT_RENDER_ASYNC) frames rotate over the slots, each with its own stream, so one frame's
@@ -1364,7 +1365,10 @@ struct srt_ctx {
     // their own ("copy_stream").  ex1 1080p, host outputs, one MI355X, ms/frame: 3 slots 1.83; 2 slots
     // + copy stream 1.83; 3 slots + MT stream 1.82; 2 slots 2.20; 2 slots + MT stream 2.00; one rank's
     // shard of an 8-GPU frame (bench --shard-of 8, same box): 3 slots 0.627, 4 slots 0.544, 3 slots +
-    // MT stream 0.857.  Four slots (a stream each, HIP's default of four hardware queues per process)
+    // MT stream 0.857.  Default (default_slots): one slot per hardware queue HIP gives the process
+    // but one, at least four: GPU_MAX_HW_QUEUES=7 (bench.py sets it) -> 6 slots: one rank of 8,
+    // slowest rank 0.318 -> 0.265 ms per frame, the whole ex1 frame 1.30 -> 1.26 ms (8 slots: 0.41 /
+    // 1.28; profiles/r03_slots_ab.txt)
     int nslots = 4;
     // -1 auto: a high-priority stream of its own for frames of more than a third of the rows (ex1 1080p
     // 1.80 -> 1.64 ms/frame, same box; one rank of 2: 0.989 -> 0.926 ms), the frame's stream for
@@ -2051,11 +2055,20 @@ int srt_device_count(int* count) {
     return SRT_OK;
 }
 
+// frame slots by default: HIP's hardware queues per process (GPU_MAX_HW_QUEUES, default 4) but one
+// for the generation stream, at least 4, at most MAX_FRAME_SLOTS
+static int default_slots() {
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    const int q = e ? atoi(e) : 4;
+    return std::max(4, std::min(MAX_FRAME_SLOTS, q - 1));
+}
+
 int srt_create(int device, srt_ctx** out) {
     if (!out) return fail(SRT_ERR_ARG, "out is null");
     *out = nullptr;
     HIP_TRY(hipSetDevice(device));
     srt_ctx* c = new srt_ctx();
+    c->nslots = default_slots();
     c->device = device;
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -2142,7 +2155,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         return SRT_OK;
     }
     if (!strcmp(key, "slots") || !strcmp(key, "mt_stream") || !strcmp(key, "copy_stream")) {
-        if (!strcmp(key, "slots") && (value < 1 || value > MAX_FRAME_SLOTS)) return fail(SRT_ERR_ARG, "slots: 1..4");
+        if (!strcmp(key, "slots") && (value < 1 || value > MAX_FRAME_SLOTS)) return fail(SRT_ERR_ARG, "slots: 1..8");
         HIP_TRY(hipSetDevice(c->device));
         int rc = finish_async(c, nullptr);  // the frames in flight finish on the old arrangement
         if (rc) return rc;
