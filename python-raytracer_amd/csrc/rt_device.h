@@ -1120,7 +1120,11 @@ RT_HD uint32_t child_path(uint32_t path, uint32_t slot, uint32_t round) { return
 // as the balance allows: h is chosen per (H, n) with at most `kmax` bands per rank (and at least
 // kmax / 2), the fewest rows on the busiest rank first, then the most bands.
 constexpr int SHARD_BANDS = 8;  // kmax: most bands per rank (option "shard_bands"; 0 = shard_kmax's choice)
-constexpr int SHARD_SNAKE = 1;  // dealing order (option "shard_snake")
+// dealing order (option "shard_snake"): round-robin.  A snake deals two adjacent bands to the first
+// and the last rank at every turn, one run of the numpy stream twice as long to generate: ex1 1080p,
+// slowest of 8 ranks 0.317 (snake) vs 0.288 ms (round-robin), ex4 4K 2.47 vs 2.35 ms
+// (profiles/r03_band_order_ab.txt)
+constexpr int SHARD_SNAKE = 0;
 // A Diffuse fan-out scene costs ~50 rays per pixel and sample, so a jump is a fraction of one row's
 // work and the balance wins: bands of SHARD_FANOUT_ROWS rows (cornell 800x800 on 8 ranks, slowest
 // rank of the same frame: 618 ms with 20-row bands, 583 with 4, 570 with 2; profiles/r03_*)

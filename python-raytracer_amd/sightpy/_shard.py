@@ -19,7 +19,7 @@ fan-out scene, whose rows cost ~30x more, takes 2-row bands (shard_kmax).
 import numpy as np
 
 SHARD_BANDS = 8  # kmax (library option "shard_bands"; 0 = shard_kmax's choice)
-SHARD_SNAKE = 1  # dealing order (library option "shard_snake")
+SHARD_SNAKE = 0  # dealing order (library option "shard_snake")
 SHARD_FANOUT_ROWS = 2  # band rows of a Diffuse fan-out scene (rt_device.h shard_kmax)
 
 

@@ -62,8 +62,11 @@ def test_shard_rows_partition():
     assert list(shard_rows(40, 2, 0, kmax=2, snake=0)) == list(range(0, 10)) + list(range(20, 30))
 
 
-def _kernel_shard_map(H, n, kmax=8, snake=1):
+def _kernel_shard_map(H, n, kmax=8, snake=None):
     import hostcheck as HC
+    from sightpy._shard import SHARD_SNAKE
+
+    snake = SHARD_SNAKE if snake is None else snake
 
     owner = np.empty(H, dtype=np.int32)
     local = np.empty(H, dtype=np.int64)
