@@ -2558,7 +2558,12 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (use_mt) {
             // (more than a third of the rows: whole frames and both ranks of a 2-rank frame, whose
             // shards differ by a band)
-            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream : (3 * (int64_t)n_rows > Hf ? 2 : 0);
+            // (auto: whole frames on the high-priority stream; a shard of more than a third of the
+            // rows -- a rank of 2 -- on a stream of its own at normal priority: 6 slots, same box,
+            // slowest of 2 ranks 0.79 / 0.79 ms vs 0.71 / 1.07 on the high-priority one and 1.08 / 1.07
+            // on the frame's stream, profiles/r03_mt_stream_ab.txt)
+            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream
+                                                  : (n_rows >= Hf ? 2 : (3 * (int64_t)n_rows > Hf ? 1 : 0));
             if (F.npass == 1 && mts) {
                 if (!c->mt_stream) {
                     // a high-priority queue (mt_stream 2): the generation's blocks are dispatched ahead
