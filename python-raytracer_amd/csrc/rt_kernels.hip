@@ -28,6 +28,7 @@
 #include <deque>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "rt_bvh.h"
@@ -334,6 +335,12 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
     }
 }
 
+// an emitter whose child replaces the traced ray in place (Em::kInPlace)
+template <class Em, class = void>
+struct em_in_place : std::false_type {};
+template <class Em>
+struct em_in_place<Em, std::void_t<decltype(Em::kInPlace)>> : std::bool_constant<Em::kInPlace> {};
+
 // One trace step for one ray (all lanes of the wave call it; `active` masks the tail).
 // MATS: material types compiled into this instantiation (the host picks one covering the scene).
 // Em: the emitter (GpuEmit: wavefront queues; FrameEmit: the frame kernel's per-wave ring); `em0`
@@ -358,6 +365,12 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         }
     } else if (active) {
         id = nearest_hit<(MATS & MAT_BVH) != 0>(S, r.o, r.d, t, o, ties);
+    }
+    if constexpr (em_in_place<Em>::value) {
+        // the emitter writes the child over `r` (the fused path): no tie loop, which would read the
+        // ray after shading; a tie renders the frame again without the fused path
+        if (ties) atomicOr(&P.flags[1], RETRY_CHAIN_TIE);
+        ties = false;
     }
     RT_ACC(1, tn0);
     if (hit_slot && active) *hit_slot = id;
@@ -482,6 +495,7 @@ struct ChainEmit {
 // in the pixel's own thread): colour of every depth into the thread's register sum, the one child
 // replaces the ray.  A second child (an exact tie) raises RETRY_CHAIN_TIE as in chain mode.
 struct FusedEmit {
+    static constexpr bool kInPlace = true;  // `next` is the traced ray itself (see trace_one)
     const TraceParams& P;
     const Ray& r;
     uint32_t round;
@@ -560,9 +574,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
                 // the sample's whole path in this thread (single-child scenes): no queue, every
                 // depth's colour into `acc`; the lanes of an iteration share a depth, counted per
                 // wave into the shard's counter of that depth as the queue appends would have been
-                Ray nx = r;
+                // (the child is written over r: shading reads nothing of the ray after it)
                 bool has = false;
-                trace_one<MATS>(P, r, active, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &nx, &has});
+                trace_one<MATS>(P, r, active, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
                 bool live = active && has;
                 for (int d = 1;; ++d) {
                     const uint64_t m = __ballot(live);
@@ -570,9 +584,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
                     if (live && lanes_below(m) == 0 && d < SRT_MAX_DEPTHS)  // the lowest live lane
                         atomicAdd(P.cnt_out + (int64_t)(d - 1) * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
                     if (d > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
-                    r = nx;
                     has = false;
-                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &nx, &has});
+                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
                     live = live && has;
                 }
             }
@@ -963,7 +976,7 @@ int g_occupancy = 0;
 #endif
 constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (register cap 512 / OCC)
 #ifndef RT_FUSE_OCC
-#define RT_FUSE_OCC 2  // the fused k_primary holds the next ray as well: 45 VGPRs spilled at 3 waves/SIMD
+#define RT_FUSE_OCC 3  // waves/SIMD of the fused k_primary (the child written over the ray: 10 VGPRs spilled)
 #endif
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
