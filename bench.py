@@ -59,6 +59,8 @@ RAY_BYTES = 84  # one queued ray record (rt_kernels.hip Queue): O, D, throughput
 BYTES_MODEL = {
     "primary": "jitter read (2 f64 per sample, 4 for a thin lens) + the depth-1 children written to the queue "
                "(84 B each) + the framebuffer store (3 f64 per pixel); depth-0 rays live in registers",
+    "fused": "jitter read (2 f64 per sample, 4 for a thin lens) + the framebuffer store (3 f64) and the deeper "
+             "depths' fixed-point sums (3 x 8 B + 4 B) per pixel; every ray of every depth lives in registers",
     "frame": "jitter read + every secondary ray written to and read back from its wave's ring (2 x 84 B) + the "
              "fused resolve's uint8 and linear-RGB stores (27 B per pixel)",
 }
@@ -71,6 +73,8 @@ def kernel_bytes_model(stats, spp, npix, lens):
     rpd = stats["rays_per_depth"]
     if stats["kernel_path"] == "frame":
         return spp * npix * planes * 8 + sum(rpd[1:]) * 2 * RAY_BYTES + npix * 27
+    if stats["kernel_path"] == "fused":
+        return spp * npix * planes * 8 + npix * (24 + 28)
     children = rpd[1] if len(rpd) > 1 else 0
     return spp * npix * planes * 8 + children * RAY_BYTES + npix * 24
 
@@ -196,7 +200,7 @@ def cpu_baseline(builder, W, H, depth, spp, frame_rays, tile_of=0, budget_s=15.0
     return one
 
 
-def pmc_counters(config, kernel):
+def pmc_counters(config, kernel, variant=None):
     """Per-launch counters of `kernel` from the newest committed PMC summary of this config
     (profiles/rNN_counters_<config>.json, tools/pmc_summary.py over separate rocprofv3 --pmc passes of
     this bench: FETCH_SIZE, WRITE_SIZE, SQ fp64/VALU/wait counters), or (None, None)."""
@@ -205,12 +209,12 @@ def pmc_counters(config, kernel):
         return None, None
     rec = json.loads(files[-1].read_text())
     for name, k in rec["kernels"].items():
-        if kernel in name:
+        if kernel in name and (variant is None or variant in name):
             return k, files[-1].name
     return None, None
 
 
-def roofline(kname, kms, model_bytes, frame_path, krec, src):
+def roofline(kname, kms, model_bytes, path, krec, src):
     """The dominant kernel against the MI355X roofline.  achieved = algorithmic bytes / launch time
     (HIP events); traffic = PMC HBM bytes per launch; the arithmetic intensity (counted fp64 FLOP per
     PMC byte) against the ridge (78.6 TF / 8 TB/s) classifies the bound; the counters then say what
@@ -219,7 +223,7 @@ def roofline(kname, kms, model_bytes, frame_path, krec, src):
     roof = {"kernel": kname, "kernel_ms": round(kms, 4), "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
             "achieved": round(model_bytes / sec / 1e9, 2), "frac": round(model_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
             "algorithmic_GB_per_launch": round(model_bytes / 1e9, 4),
-            "bytes_model": BYTES_MODEL["frame" if frame_path else "primary"], "traffic": None}
+            "bytes_model": BYTES_MODEL[path], "traffic": None}
     if krec is None or "traffic_bytes" not in krec:
         return roof
     tb = krec["traffic_bytes"]
@@ -233,11 +237,16 @@ def roofline(kname, kms, model_bytes, frame_path, krec, src):
         ai = krec["fp64_flop"] / tb
         ridge = FP64_PEAK_TFS * 1e3 / HBM_PEAK_GBS
         tf = krec["fp64_flop"] / sec / 1e12
-        roof["bound"] = "hbm" if ai < ridge else "fp64-valu"
         roof["arith_intensity_flop_per_byte"] = round(ai, 2)
         roof["ridge_flop_per_byte"] = round(ridge, 2)
         roof["fp64"] = {"achieved_TFLOPs": round(tf, 3), "peak": FP64_PEAK_TFS, "frac": round(tf / FP64_PEAK_TFS, 4),
                         "note": "64 x (ADD + MUL + TRANS + 2 FMA) f64 wave instructions: counts masked lanes"}
+        if ai >= ridge:
+            # the fp64 side of the ridge: the kernel is measured against the vector fp64 peak (there is
+            # no MFMA work here); the HBM figures stay beside it
+            roof["hbm"] = {k: roof[k] for k in ("achieved", "peak", "unit", "frac")}
+            roof.update({"bound": "fp64", "achieved": round(tf, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP64_PEAK_TFS, 4)})
     # (tools/pmc_summary.py: VALU issue cycles over the dispatch's SIMD cycles, GRBM_GUI_ACTIVE / 8 XCDs)
     if krec.get("valu_issue_frac") is not None:
         roof["valu_issue_frac"] = round(krec["valu_issue_frac"], 4)
@@ -602,20 +611,21 @@ def main():
             if "device_resident" in sec:
                 rec["device_resident"] = sec["device_resident"]
             st0 = sec["stats"]
-            frame_path = st0[0]["kernel_path"] == "frame"
+            path = {"frame": "frame", "fused": "fused"}.get(st0[0]["kernel_path"], "primary")
+            frame_path = path == "frame"
             kname = "k_frame" if frame_path else "k_primary"
             # one launch of the dominant kernel: a frame of `passes` passes launches it once per pass
             npass = max(1, st0[0]["passes"])
             kms = float(np.mean([x["ms_primary_kernel"] for x in st0])) / npass
             krec, src = (None, None) if (args.size or args.spp or world > 1 or rows32 is not None) else \
-                pmc_counters(args.config, kname)
+                pmc_counters(args.config, kname, {"fused": ", true>", "primary": ", false>"}.get(path))
             from sightpy._shard import shard_rows
 
             npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0, kmax, snake)) * W
             st_pass = dict(st0[0])
             st_pass["rays_per_depth"] = [r / npass for r in st0[0]["rays_per_depth"]]
             model = kernel_bytes_model(st_pass, spp / npass, npix_rank, sc.camera.lens_radius != 0.0)
-            roof = roofline(kname, kms, model, frame_path, krec, src)
+            roof = roofline(kname + (" (fused paths)" if path == "fused" else ""), kms, model, path, krec, src)
             if npass > 1:
                 roof["passes_per_frame"] = npass
             roof["kernel_ms_note"] = ("one launch in a synchronous frame (HIP events); pipelined frames overlap one "

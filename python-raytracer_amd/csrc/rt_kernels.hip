@@ -492,8 +492,13 @@ struct ChainEmit {
 };
 
 // Fused-path emitter (k_primary<.., FUSE>: single-child scenes traced pixel by pixel, every depth
-// in the pixel's own thread): colour of every depth into the thread's register sum, the one child
-// replaces the ray.  A second child (an exact tie) raises RETRY_CHAIN_TIE as in chain mode.
+// in the pixel's own thread): the one child replaces the ray.  A second child (an exact tie) raises
+// RETRY_CHAIN_TIE as in chain mode.
+// Deeper depths' colour summed in the thread as the framebuffer's fixed-point terms (integer sums:
+// the same totals as one atomic per term), added to it once per pixel.
+struct FxAcc {
+    long long x = 0, y = 0, z = 0;
+};
 struct FusedEmit {
     static constexpr bool kInPlace = true;  // `next` is the traced ray itself (see trace_one)
     const TraceParams& P;
@@ -503,9 +508,24 @@ struct FusedEmit {
     d3* acc;
     Ray* next;
     bool* has;
+    FxAcc* fx;
 
+    // depth 0 into the thread's register sum, deeper depths into the framebuffer's order-independent
+    // fixed-point sums exactly as the per-depth kernels add them: the fused and the wavefront paths
+    // give the same image bit for bit
     __device__ void local(d3 c) const {
-        if (!is_zero(c)) *acc = add(*acc, mul(r.w, c));
+        if (is_zero(c)) return;
+        if (meta_depth(r.meta) == 0) {
+            *acc = add(*acc, mul(r.w, c));
+        } else if (P.fbx) {  // fb_add's terms, summed here
+            // (terms are non-negative: a term out of range, or NaN, leaves its sum out of range, which
+            // the thread checks once at the end)
+            fx->x += __double2ll_rn((r.w.x * c.x) * FX_SCALE);
+            fx->y += __double2ll_rn((r.w.y * c.y) * FX_SCALE);
+            fx->z += __double2ll_rn((r.w.z * c.z) * FX_SCALE);
+        } else {
+            fb_add(P.fb, P.fbx, P.flags, P.npix, r.pix, r.w, c);
+        }
     }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void child(const Child& c) const {
@@ -551,6 +571,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         const double xc = active ? P.cam.xs[col] : 0.0, yr = active ? P.cam.ys[grow] : 0.0;
         d3 acc = d3{0.0, 0.0, 0.0};
         const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
+        FxAcc fxa;
         // software pipeline: the next sample's uniforms are loaded while this sample is traced
         double jn[4] = {0.0, 0.0, 0.0, 0.0};
         if (active) primary_uniforms(P, s_begin, p, gpix, jn);
@@ -576,7 +597,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
                 // wave into the shard's counter of that depth as the queue appends would have been
                 // (the child is written over r: shading reads nothing of the ray after it)
                 bool has = false;
-                trace_one<MATS>(P, r, active, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
+                trace_one<MATS>(P, r, active, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has, &fxa});
                 bool live = active && has;
                 for (int d = 1;; ++d) {
                     const uint64_t m = __ballot(live);
@@ -585,7 +606,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
                         atomicAdd(P.cnt_out + (int64_t)(d - 1) * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
                     if (d > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
                     has = false;
-                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
+                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has, &fxa});
                     live = live && has;
                 }
             }
@@ -606,6 +627,29 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             P.fb[p] += acc.x;
             P.fb[P.npix + p] += acc.y;
             P.fb[2 * P.npix + p] += acc.z;
+        }
+        if (FUSE && active && P.fbx) {
+            // the deeper depths' fixed-point terms of this thread's samples (after the first pass's
+            // store above started the pixel's sums; other threads of a split pixel add theirs too)
+            // range: every sum in [0, 2^17) in colour units (a term of 2^17 or more, a NaN or a
+            // negative term shows here), the magnitude guard from the sums (terms are non-negative)
+            const long long lim = (long long)(FX_MAX * FX_SCALE);
+            if (!(fxa.x >= 0 && fxa.x < lim && fxa.y >= 0 && fxa.y < lim && fxa.z >= 0 && fxa.z < lim))
+                atomicOr(&P.flags[1], RETRY_FIXED_RANGE);
+            const float mag = (float)((double)((fxa.x + fxa.y) + fxa.z) * FX_UNIT);
+            if (fxa.x | fxa.y | fxa.z) {
+                if (ngroups == 1 && P.fb_first) {
+                    P.fbx[p] = (unsigned long long)fxa.x;
+                    P.fbx[P.npix + p] = (unsigned long long)fxa.y;
+                    P.fbx[2 * P.npix + p] = (unsigned long long)fxa.z;
+                    fx_mag(P.fbx, P.npix)[p] = mag;
+                } else {
+                    atomicAdd(P.fbx + p, (unsigned long long)fxa.x);
+                    atomicAdd(P.fbx + P.npix + p, (unsigned long long)fxa.y);
+                    atomicAdd(P.fbx + 2 * P.npix + p, (unsigned long long)fxa.z);
+                    unsafeAtomicAdd(fx_mag(P.fbx, P.npix) + p, mag);
+                }
+            }
         }
     }
     if (err) atomicOr(&P.flags[0], err);
@@ -1419,7 +1463,11 @@ struct srt_ctx {
     int shard_bands = 0;  // option "shard_bands": most row bands per rank (0: rt_device.h shard_kmax by the scene's fan-out)
     int shard_snake = SHARD_SNAKE;  // option "shard_snake": bands dealt in alternating direction per period
     int frame_groups = 0;           // option "frame_groups": k_frame sample groups per tile (0: auto)
-    int fuse_primary = 0;           // option "fuse_primary": single-child scenes traced whole-path per pixel in k_primary
+    // option "fuse_primary": single-child scenes traced whole-path per pixel in k_primary (same image
+    // bit for bit as the per-depth kernels); -1 (default) for frames of at least two resident
+    // rounds of threads: ex1 1080p 1.308 -> 1.209 ms per frame, a rank of 4 0.47 -> 0.44, while a rank
+    // of 8 (1.3 rounds) is faster per depth, 0.29 vs 0.35 (profiles/r03_fused_ab.txt)
+    int fuse_primary = -1;
     double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
@@ -2406,7 +2454,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         const int64_t g = c->frame_groups > 0 ? c->frame_groups : (want + ntiles - 1) / ntiles;
         F.groups = (int)std::max<int64_t>(1, std::min<int64_t>(g, batch));
     }
-    F.fuse = !F.frame && c->fanout == 1 && c->chain_ok && c->fuse_primary > 0 && pick_variant(c->mats).fused;
+    F.fuse = !F.frame && c->fanout == 1 && c->chain_ok && pick_variant(c->mats).fused &&
+             (c->fuse_primary > 0 ||
+              (c->fuse_primary < 0 && npix >= 2 * (int64_t)c->ncu * 4 * OCC * 64));
     if (!F.fuse && !F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
         c->hint_key[2] == batch) {
         for (int d = 1; d <= F.dcap; ++d)

@@ -239,7 +239,7 @@ def test_gpu_every_kernel_path_matches_reference(name, builder, depth, mode):
     finally:
         _set_option("frame_kernel", -1)
         _set_option("chain_rays", 1000000)
-        _set_option("fuse_primary", 0)
+        _set_option("fuse_primary", -1)
     if mode == "fused" and builder is scenes.example1:
         assert out.stats["kernel_path"] == "fused"
     assert np.array_equal(out.hit_ids, g["hit_id"])
