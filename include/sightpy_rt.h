@@ -56,6 +56,8 @@ extern "C" {
 #define SRT_ERR_MEMORY -4   /* queue / framebuffer allocation failed */
 #define SRT_ERR_INDEX -5    /* a table index left its array (the reference raises IndexError) */
 #define SRT_ERR_DEPTH -6    /* rays still alive after the depth cap */
+#define SRT_ERR_NAME -7     /* a Glossy hit shaded under a PointLight: the reference raises NameError
+                               (PointLight.get_L uses undefined names, sightpy/lights.py:30-31) */
 
 /* ---- scene tables --------------------------------------------------------------------- */
 enum { SRT_SPHERE = 0, SRT_PLANE = 1, SRT_CUBOID = 2, SRT_TRIANGLE = 3 };
@@ -152,7 +154,8 @@ typedef struct srt_light {
     int32_t reserved;
     double dir[3]; /* DirectionalLight.Ldir (normalised by Scene.add_DirectionalLight) */
     double color[3];
-    double pos[3]; /* PointLight.pos */
+    double pos[3]; /* PointLight.pos (kept for the record: shading a Glossy hit under a point light
+                      fails with SRT_ERR_NAME, as the reference raises NameError) */
 } srt_light;
 
 typedef struct srt_scene_desc {

@@ -76,6 +76,7 @@ constexpr double NUDGE = 0.000001;              // glossy.py:35 etc.
 // error bits raised by a kernel (folded into SRT_ERR_* by the host)
 constexpr uint32_t ERR_INDEX = 1u;      // texture/table index outside the array (IndexError)
 constexpr uint32_t ERR_UNSUPPORTED = 2u;  // uv of a Triangle (undefined in the reference)
+constexpr uint32_t ERR_NAME = 4u;         // a PointLight met by a Glossy hit (NameError in the reference)
 
 struct d3 {
     double x, y, z;
@@ -785,19 +786,16 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
     uint32_t med = meta_medium(r.meta);
     for (int l = 0; l < S.nlights; ++l) {
         const RT_RO srt_light& Lt = S.lights[l];
-        d3 L, lv;
-        double dist;
-        if (Lt.type == SRT_LIGHT_DIRECTIONAL) {
-            L = ld3(Lt.dir);
-            dist = SKYBOX_DISTANCE;
-        } else {  // point light, evident intent of lights.py:23-37 (parity unpinned)
-            d3 toL = sub(ld3(Lt.pos), P);
-            dist = sqrt(dot(toL, toL));
-            L = mul(toL, 1.0 / dist);
+        if (Lt.type != SRT_LIGHT_DIRECTIONAL) {
+            // PointLight.get_L reads the undefined names M and dist_light (lights.py:30-31): the
+            // reference's render raises NameError at the first Glossy hit, so does this one
+            err |= ERR_NAME;
+            continue;
         }
+        const d3 L = ld3(Lt.dir);
+        const double dist = SKYBOX_DISTANCE;
         double NdotL = np_max(dot(N, L), 0.0);
-        lv = mul(ld3(Lt.color), NdotL);
-        if (Lt.type != SRT_LIGHT_DIRECTIONAL) lv = mul(divs(lv, dist * dist), 100.0);
+        const d3 lv = mul(ld3(Lt.color), NdotL);
         d3 H = normalize(add(L, V));
         double seelight = 1.0;
 #ifdef RT_ABL_SHADOW  // diagnostic build only: time without the shadow test

@@ -141,6 +141,7 @@ void trace_one(const SceneView& S, const Ray& r, int depth, uint64_t seed, std::
 int err_code(uint32_t e) {
     if (e & ERR_INDEX) { g_err = "index out of bounds in a texture/table lookup"; return SRT_ERR_INDEX; }
     if (e & ERR_UNSUPPORTED) { g_err = "uv requested on a Triangle"; return SRT_ERR_ARG; }
+    if (e & ERR_NAME) { g_err = "name 'M' is not defined (PointLight.get_L)"; return SRT_ERR_NAME; }
     return SRT_OK;
 }
 

@@ -101,8 +101,7 @@ struct TraceParams {
     int jit_global;        // 1: jitter indexed by the global pixel (the whole frame's numpy stream)
     int sample_base;
     int spp;           // samples of this pass (k_primary)
-    int spt;           // samples per thread: k_primary item i = (pixel i % npix, samples [g*spt, g*spt+spt)),
-                       // g = i / npix; spt < spp (small frames) adds to a zeroed framebuffer with atomics
+    int pix_groups;    // k_primary: sample groups per pixel (a power of two <= 64; lanes of one wave)
     int chain;         // k_trace: trace each ray's whole (single-child) chain in-thread, see k_trace
     int32_t* hit_out;  // [spp][npix] or null
     // frame kernel (k_frame): per-wave ray rings in HBM, slot s = rays [s * ring_cap, (s+1) * ring_cap)
@@ -257,6 +256,57 @@ __device__ __forceinline__ uint32_t wave_below(uint32_t cnt) {
     return below;
 }
 
+// A pixel's colour summed in the thread that traces (some of) its samples, in one of two forms
+// sharing the same registers:
+//  * fixed point (P.fbx set, the default): every term -- depth 0 included -- rounded to a multiple of
+//    2^-FX_BITS and summed as an integer (unsigned: wrapping is defined), exactly fb_add's terms, plus
+//    fb_add's coarse magnitude (the f32 sum of |r| + |g| + |b| of the terms, independent of the sums).
+//    Integer sums do not depend on the order or grouping of the terms, so a pixel's samples may be
+//    split over any number of threads (sample groups, k_primary) or GPUs and the totals are the same
+//    bits.  A term of magnitude >= 2^17 (or NaN) is left out of the sums and shows in the magnitude
+//    (>= FX_MAG_LIMIT or NaN): the frame is then rendered again in f64.
+//  * f64 (option deterministic 0, or that fallback): the f64 sums, in the words' bits.
+struct PixAcc {
+    unsigned long long w[3] = {0ull, 0ull, 0ull};
+    float mag = 0.0f;
+
+    __device__ __forceinline__ void add(bool fx, d3 t) {
+        if (fx) {
+            const double m = (fabs(t.x) + fabs(t.y)) + fabs(t.z);
+            if (m < FX_MAX) {  // every |term| < 2^17: the conversions are in range (NaN fails too)
+                w[0] += (unsigned long long)__double2ll_rn(t.x * FX_SCALE);
+                w[1] += (unsigned long long)__double2ll_rn(t.y * FX_SCALE);
+                w[2] += (unsigned long long)__double2ll_rn(t.z * FX_SCALE);
+            }
+            mag += (float)m;
+        } else {
+            w[0] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)w[0]) + t.x);
+            w[1] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)w[1]) + t.y);
+            w[2] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)w[2]) + t.z);
+        }
+    }
+    __device__ __forceinline__ double value(bool fx, int k) const {
+        return fx ? (double)(long long)w[k] * FX_UNIT : __longlong_as_double((long long)w[k]);
+    }
+    // the pixel's fixed-point totals the resolve must not trust (fx_suspect's rule)
+    __device__ __forceinline__ bool suspect() const {
+        return !(mag < FX_MAG_LIMIT) || ((w[0] | w[1] | w[2]) >> 61) != 0;
+    }
+    // sum over the lanes l ^ off, off = 32, 16, .. >= lo (the sample groups of a pixel, k_primary):
+    // integer sums exactly; f64 sums pairwise, commutative, so every lane ends with the same value
+    __device__ __forceinline__ void reduce_lanes(bool fx, int lo) {
+        for (int off = 32; off >= lo; off >>= 1) {
+            for (int k = 0; k < 3; ++k) {
+                const unsigned long long o = __shfl_xor(w[k], off);
+                w[k] = fx ? w[k] + o
+                          : (unsigned long long)__double_as_longlong(__longlong_as_double((long long)w[k]) +
+                                                                     __longlong_as_double((long long)o));
+            }
+            mag += __shfl_xor(mag, off);
+        }
+    }
+};
+
 // Emitter of the GPU trace step: colour -> framebuffer atomics, children -> output queue shard.
 struct GpuEmit {
     const TraceParams& P;
@@ -264,11 +314,11 @@ struct GpuEmit {
     uint32_t shard;
     uint32_t round;
     uint32_t* shadow_acc;
-    d3* acc;  // depth 0: the pixel's register accumulator (no framebuffer atomics)
+    PixAcc* acc;  // depth 0: the pixel's sums in the thread (no framebuffer atomics)
 
     __device__ void local(d3 c) const {
         if (acc) {
-            if (!is_zero(c)) *acc = add(*acc, mul(r.w, c));
+            if (!is_zero(c)) acc->add(P.fbx != nullptr, mul(r.w, c));
         } else {
             fb_add(P.fb, P.fbx, P.flags, P.npix, r.pix, r.w, c);
         }
@@ -493,39 +543,22 @@ struct ChainEmit {
 
 // Fused-path emitter (k_primary<.., FUSE>: single-child scenes traced pixel by pixel, every depth
 // in the pixel's own thread): the one child replaces the ray.  A second child (an exact tie) raises
-// RETRY_CHAIN_TIE as in chain mode.
-// Deeper depths' colour summed in the thread as the framebuffer's fixed-point terms (integer sums:
-// the same totals as one atomic per term), added to it once per pixel.
-struct FxAcc {
-    long long x = 0, y = 0, z = 0;
-};
+// RETRY_CHAIN_TIE as in chain mode.  Every depth's colour goes into the thread's PixAcc: the same
+// fixed-point terms the per-depth kernels add (their k_primary keeps depth 0 in a PixAcc, k_trace
+// adds the deeper terms with fb_add), so the fused and the per-depth paths give the same image bit
+// for bit; in f64 mode the terms are summed in the thread in trace order.
 struct FusedEmit {
     static constexpr bool kInPlace = true;  // `next` is the traced ray itself (see trace_one)
     const TraceParams& P;
     const Ray& r;
     uint32_t round;
     uint32_t* shadow_acc;
-    d3* acc;
+    PixAcc* acc;
     Ray* next;
     bool* has;
-    FxAcc* fx;
 
-    // depth 0 into the thread's register sum, deeper depths into the framebuffer's order-independent
-    // fixed-point sums exactly as the per-depth kernels add them: the fused and the wavefront paths
-    // give the same image bit for bit
     __device__ void local(d3 c) const {
-        if (is_zero(c)) return;
-        if (meta_depth(r.meta) == 0) {
-            *acc = add(*acc, mul(r.w, c));
-        } else if (P.fbx) {  // fb_add's terms, summed here
-            // (terms are non-negative: a term out of range, or NaN, leaves its sum out of range, which
-            // the thread checks once at the end)
-            fx->x += __double2ll_rn((r.w.x * c.x) * FX_SCALE);
-            fx->y += __double2ll_rn((r.w.y * c.y) * FX_SCALE);
-            fx->z += __double2ll_rn((r.w.z * c.z) * FX_SCALE);
-        } else {
-            fb_add(P.fb, P.fbx, P.flags, P.npix, r.pix, r.w, c);
-        }
+        if (!is_zero(c)) acc->add(P.fbx != nullptr, mul(r.w, c));
     }
     __device__ void shadow(int n) const { *shadow_acc += (uint32_t)n; }
     __device__ void child(const Child& c) const {
@@ -536,9 +569,6 @@ struct FusedEmit {
     }
 };
 
-// Depth 0: one thread per pixel walks the pass's samples, generating each primary ray
-// (camera.py:51-85) and tracing it; the pixel's depth-0 colour is summed in registers and added to
-// the framebuffer once (no other thread touches the pixel during this launch).
 // Copy the first `nlut` texture lookup tables into LDS (dynamic shared memory) and point the
 // scene view at them: texel -> value becomes an LDS read instead of a dependent global load.
 __device__ __forceinline__ void stage_luts(TraceParams& P) {
@@ -549,6 +579,33 @@ __device__ __forceinline__ void stage_luts(TraceParams& P) {
     __syncthreads();
 }
 
+// The uint8 RGB of n consecutive pixels (lane l < n holds pixel p0 + l; dst = out + 3 p0) as 3n/4
+// dword stores instead of 3n byte stores (n a multiple of 4, dst 4-byte aligned); otherwise byte
+// stores.  Every lane of the wave must call it (cross-lane reads).
+__device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3], int lane, int n) {
+    const uint32_t v = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+    if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+        const int nd = (3 * n) / 4;
+        const int w = lane < nd ? lane : nd - 1;
+        const int q0 = (4 * w) / 3, r0 = (4 * w) % 3;  // dword w = bytes 4w..4w+3: pixels q0, q0 + 1
+        const uint32_t x0 = __shfl(v, q0), x1 = __shfl(v, q0 + 1);
+        if (lane < nd) reinterpret_cast<uint32_t*>(dst)[lane] = (x0 >> (8 * r0)) | (x1 << (8 * (3 - r0)));
+    } else if (lane < n) {
+        dst[3 * lane] = px[0];
+        dst[3 * lane + 1] = px[1];
+        dst[3 * lane + 2] = px[2];
+    }
+}
+
+// Depth 0: primary-ray generation (camera.py:51-85) fused with the trace step.  A wave takes
+// ppw = 64 / G consecutive pixels of the pass: lane l traces pixel l % ppw through the samples of
+// its sample group l / ppw (G = P.pix_groups, a power of two; G > 1 gives a small frame -- one GPU's
+// shard of a multi-GPU frame -- enough threads to fill the GPU).  A pixel's colour is summed in the
+// thread (PixAcc), its groups combined by lane shuffles, and its lane of group 0 stores the pixel:
+// no framebuffer atomics, no memset.  FUSE (single-child scenes): every depth of the sample's path
+// is traced in the thread too (no ray queues), and a single-pass frame resolves the pixel here
+// (P.fuse_resolve: average, sRGB, uint8; no framebuffer at all).  Otherwise the children are appended
+// to the depth-1 queue for k_trace.
 template <uint32_t MATS, int OCC = 2, bool FUSE = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     TraceParams P = P0;
@@ -556,26 +613,31 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
     uint32_t shadow = 0;
-    const int64_t ngroups = (P.spp + P.spt - 1) / P.spt;
-    const int64_t n = P.npix * ngroups;
+    const bool fx = P.fbx != nullptr;
+    const int ppw = 64 / P.pix_groups;  // pixels per wave
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / ppw;
+    const int spg = (P.spp + P.pix_groups - 1) / P.pix_groups;
+    const int s_begin = min(P.spp, grp * spg), s_end = min(P.spp, s_begin + spg);
+    const int64_t nwaves = (P.npix + ppw - 1) / ppw;
     const Quot qw((double)P.cam.width), qh((double)P.cam.height);
-    for (int64_t base = (int64_t)blockIdx.x * BLOCK; base < n; base += (int64_t)gridDim.x * BLOCK) {
-        const int64_t i = base + threadIdx.x;
-        const bool active = i < n;
-        const int64_t grp = active ? i / P.npix : 0;
-        const uint32_t p = active ? (uint32_t)(i - grp * P.npix) : 0u;
-        const int s_begin = (int)grp * P.spt, s_end = min(P.spp, s_begin + P.spt);
-        const uint32_t lr = p / (uint32_t)P.cam.width;
-        const uint32_t col = p - lr * (uint32_t)P.cam.width;
-        const int grow = active ? P.rows[lr] : 0;
-        const double xc = active ? P.cam.xs[col] : 0.0, yr = active ? P.cam.ys[grow] : 0.0;
-        d3 acc = d3{0.0, 0.0, 0.0};
+    for (int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); wv < nwaves;
+         wv += (int64_t)gridDim.x * (BLOCK / 64)) {
+        const int64_t p0 = wv * ppw;
+        const uint32_t p = (uint32_t)(p0 + (lane & (ppw - 1)));
+        const bool pact = p < (uint64_t)P.npix;
+        const bool active = pact && s_begin < s_end;
+        const uint32_t lr = pact ? p / (uint32_t)P.cam.width : 0u;
+        const uint32_t col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
+        const int grow = pact ? P.rows[lr] : 0;
+        const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
         const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
-        FxAcc fxa;
+        const int s_stop = active ? s_end : s_begin;  // (no samples for a lane past the frame's end)
+        PixAcc acc;
         // software pipeline: the next sample's uniforms are loaded while this sample is traced
         double jn[4] = {0.0, 0.0, 0.0, 0.0};
         if (active) primary_uniforms(P, s_begin, p, gpix, jn);
-        for (int s = s_begin; s < s_end; ++s) {
+        for (int s = s_begin; s < s_stop; ++s) {
             Ray r;
             r.o = r.d = d3{0.0, 0.0, 0.0};
             r.w = d3{1.0, 1.0, 1.0};
@@ -584,21 +646,21 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
             const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
             RT_T0(tr0);
-            if (active && s + 1 < s_end) primary_uniforms(P, s + 1, p, gpix, jn);
-            if (active) primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
+            if (s + 1 < s_stop) primary_uniforms(P, s + 1, p, gpix, jn);
+            primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
             RT_ACC(0, tr0);
             int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
             RT_T0(tt0);
             if (!FUSE) {
-                trace_one<MATS>(P, r, active, err, hs, GpuEmit{P, r, shard, 0u, &shadow, &acc});
+                trace_one<MATS>(P, r, true, err, hs, GpuEmit{P, r, shard, 0u, &shadow, &acc});
             } else {
                 // the sample's whole path in this thread (single-child scenes): no queue, every
                 // depth's colour into `acc`; the lanes of an iteration share a depth, counted per
                 // wave into the shard's counter of that depth as the queue appends would have been
                 // (the child is written over r: shading reads nothing of the ray after it)
                 bool has = false;
-                trace_one<MATS>(P, r, active, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has, &fxa});
-                bool live = active && has;
+                trace_one<MATS>(P, r, true, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
+                bool live = has;
                 for (int d = 1;; ++d) {
                     const uint64_t m = __ballot(live);
                     if (m == 0) break;
@@ -606,49 +668,51 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
                         atomicAdd(P.cnt_out + (int64_t)(d - 1) * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
                     if (d > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
                     has = false;
-                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has, &fxa});
+                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
                     live = live && has;
                 }
             }
             RT_ACC(3, tt0);
         }
-        if (ngroups > 1) {
-            if (active) fb_add(P.fb, P.fbx, P.flags, P.npix, p, d3{1.0, 1.0, 1.0}, acc);
-        } else if (active && P.fb_first) {
-            P.fb[p] = acc.x;
-            P.fb[P.npix + p] = acc.y;
-            P.fb[2 * P.npix + p] = acc.z;
-            if (P.fbx) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = 0ull;  // this frame's fixed-point sums start here
-                fx_mag(P.fbx, P.npix)[p] = 0.0f;
-            }
-        } else if (active && !is_zero(acc)) {
-            P.fb[p] += acc.x;
-            P.fb[P.npix + p] += acc.y;
-            P.fb[2 * P.npix + p] += acc.z;
-        }
-        if (FUSE && active && P.fbx) {
-            // the deeper depths' fixed-point terms of this thread's samples (after the first pass's
-            // store above started the pixel's sums; other threads of a split pixel add theirs too)
-            // range: every sum in [0, 2^17) in colour units (a term of 2^17 or more, a NaN or a
-            // negative term shows here), the magnitude guard from the sums (terms are non-negative)
-            const long long lim = (long long)(FX_MAX * FX_SCALE);
-            if (!(fxa.x >= 0 && fxa.x < lim && fxa.y >= 0 && fxa.y < lim && fxa.z >= 0 && fxa.z < lim))
-                atomicOr(&P.flags[1], RETRY_FIXED_RANGE);
-            const float mag = (float)((double)((fxa.x + fxa.y) + fxa.z) * FX_UNIT);
-            if (fxa.x | fxa.y | fxa.z) {
-                if (ngroups == 1 && P.fb_first) {
-                    P.fbx[p] = (unsigned long long)fxa.x;
-                    P.fbx[P.npix + p] = (unsigned long long)fxa.y;
-                    P.fbx[2 * P.npix + p] = (unsigned long long)fxa.z;
-                    fx_mag(P.fbx, P.npix)[p] = mag;
-                } else {
-                    atomicAdd(P.fbx + p, (unsigned long long)fxa.x);
-                    atomicAdd(P.fbx + P.npix + p, (unsigned long long)fxa.y);
-                    atomicAdd(P.fbx + 2 * P.npix + p, (unsigned long long)fxa.z);
-                    unsafeAtomicAdd(fx_mag(P.fbx, P.npix) + p, mag);
+        // the pixel's sample groups (lanes of this wave) summed; lane of group 0 stores the pixel
+        acc.reduce_lanes(fx, ppw);
+        const bool owner = pact && grp == 0;
+        if (FUSE && P.fuse_resolve) {
+            // the frame's only pass: the pixel is complete (scene.py:118-140, k_resolve's rule)
+            uint8_t px[3] = {0, 0, 0};
+            if (owner) {
+                if (fx && acc.suspect()) atomicOr(&P.flags[1], RETRY_FIXED_RANGE);
+                const double spp = (double)P.spp_total;
+                const double rr = acc.value(fx, 0) / spp, gg = acc.value(fx, 1) / spp, bb = acc.value(fx, 2) / spp;
+                double a0, a1, a2;
+                resolve_pixel(rr, gg, bb, a0, a1, a2, px);
+                if (P.out_rgb) {
+                    P.out_rgb[p] = rr;
+                    P.out_rgb[P.npix + p] = gg;
+                    P.out_rgb[2 * P.npix + p] = bb;
                 }
+            }
+            if (P.out_u8) store_u8_chunk(P.out_u8 + 3 * p0, px, lane, (int)min<int64_t>(ppw, P.npix - p0));
+        } else if (owner && fx) {
+            // the frame's fixed-point sums (k_trace adds the deeper depths of the per-depth path);
+            // no other thread of this launch touches the pixel
+            float* mg = fx_mag(P.fbx, P.npix) + p;
+            if (P.fb_first) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = acc.w[k];
+                *mg = acc.mag;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] += acc.w[k];
+                *mg += acc.mag;
+            }
+        } else if (owner) {
+            if (P.fb_first) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] = acc.value(false, k);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] += acc.value(false, k);
             }
         }
     }
@@ -749,23 +813,6 @@ __global__ __launch_bounds__(BLOCK) void k_shade_forced(TraceParams P0) {
 // kernel, and all samples of a pixel are queued together, which keeps lanes ~95 % busy
 // (simulated on the ex1 1080p path-length distribution: 94.6 % with pure chunks).
 constexpr int FRAME_BLOCK = 64;
-
-// The uint8 RGB of 64 consecutive pixels (lane l holds pixel p0 + l; dst = out + 3 p0) as 48 dword
-// stores instead of 192 byte stores.  `n` < 64 pixels (the frame's last chunk) or an unaligned dst store bytes.  Every lane
-// of the wave must call it (cross-lane reads).
-__device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3], int lane, int n) {
-    const uint32_t v = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
-    if (n == 64 && (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
-        const int w = lane < 48 ? lane : 47;
-        const int q0 = (4 * w) / 3, r0 = (4 * w) % 3;  // dword w = bytes 4w..4w+3: pixels q0, q0 + 1
-        const uint32_t x0 = __shfl(v, q0), x1 = __shfl(v, q0 + 1);
-        if (lane < 48) reinterpret_cast<uint32_t*>(dst)[lane] = (x0 >> (8 * r0)) | (x1 << (8 * (3 - r0)));
-    } else if (lane < n) {
-        dst[3 * lane] = px[0];
-        dst[3 * lane + 1] = px[1];
-        dst[3 * lane + 2] = px[2];
-    }
-}
 
 struct FrameLds {
     double acc[3][FRAME_BLOCK];  // per-pixel colour sums of the tile
@@ -1095,12 +1142,16 @@ __global__ __launch_bounds__(BLOCK) void k_resolve(const double* fb, const unsig
         const int n = (int)min<int64_t>(64, npix - p0);
         uint8_t px[3] = {0, 0, 0};
         if (p < npix) {
-            double r = fb[p], g = fb[npix + p], b = fb[2 * npix + p];
-            if (fbx) {  // the contributions added by other threads (fixed point, order-independent)
-                r += fx_value(fbx, npix, 0, p);
-                g += fx_value(fbx, npix, 1, p);
-                b += fx_value(fbx, npix, 2, p);
+            double r, g, b;
+            if (fbx) {  // every contribution as a fixed-point term (order-independent sums)
+                r = fx_value(fbx, npix, 0, p);
+                g = fx_value(fbx, npix, 1, p);
+                b = fx_value(fbx, npix, 2, p);
                 if (fx_suspect(fbx, npix, p)) shadow_host[2] = RETRY_FIXED_RANGE;  // render again with f64
+            } else {
+                r = fb[p];
+                g = fb[npix + p];
+                b = fb[2 * npix + p];
             }
             r /= spp;
             g /= spp;
@@ -1395,7 +1446,7 @@ struct srt_ctx {
         uint64_t rows_hash;
         int nseg;
         int64_t band_len, band_period;  // merged segments store k % band_period < band_len (doubles)
-        int64_t* bands;   // device [nseg][3]
+        int64_t* bands;   // device [nseg][4]
         uint32_t* polys;  // device [nseg][624]
     };
     std::deque<MtBandTab> mt_bandtabs;  // (stable addresses: frames hold pointers into it)
@@ -1590,6 +1641,9 @@ int check_flags(uint32_t f0) {
     if (f0 & ERR_INDEX)
         return fail(SRT_ERR_INDEX, "index out of bounds in a texture/table lookup (reference raises IndexError)");
     if (f0 & ERR_UNSUPPORTED) return fail(SRT_ERR_ARG, "uv requested on a Triangle (undefined in the reference)");
+    if (f0 & ERR_NAME)
+        return fail(SRT_ERR_NAME, "name 'M' is not defined (PointLight.get_L at a Glossy hit, as the reference "
+                                  "sightpy/lights.py:30-31 raises)");
     return SRT_OK;
 }
 
@@ -1607,6 +1661,18 @@ TraceParams base_params(srt_ctx* c, uint64_t seed) {
 // (a child is made only while depth < max_ray_depth, so depth max_ray_depth is the last with rays;
 // Diffuse bounces ignore max_ray_depth (diffuse.py:25-124) and add at most two more)
 int depth_cap(const srt_ctx* c) { return std::min(SRT_MAX_DEPTHS - 2, c->max_depth + (c->has_diffuse ? 2 : 0)); }
+
+// threads the fused paths want per pass: two rounds of the resident threads (4 SIMDs x OCC waves per CU)
+int64_t fused_items(const srt_ctx* c) { return 2 * (int64_t)c->ncu * 4 * OCC * 64; }
+
+// k_primary's sample groups per pixel (TraceParams::pix_groups): the fewest (a power of two, at most
+// the pass's samples and 64) that give the pass enough threads
+int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
+    const int64_t want = fused ? fused_items(c) : (int64_t)c->max_blocks * 64;
+    int g = 1;
+    while (g * 2 <= std::min(ns, 64) && npix * g < want) g *= 2;
+    return g;
+}
 
 size_t lut_bytes(const srt_ctx* c) { return (size_t)c->S.nlut_lds * 256 * sizeof(double); }
 
@@ -1726,11 +1792,16 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
     // saves (same box, ms per rank-frame, ex1 1080p, unmerged vs merged: N = 2 1.076 vs 0.991, N = 4
     // 0.579 vs 0.614, N = 8 0.339 vs 0.422)
     const bool regular_ok = rper > rlen && rper - rlen <= rlen;
-    std::vector<int64_t> segs;  // (first double, doubles, masked)
+    // local row of each run's first row (the shard's compact jitter layout [s][plane][rows][W])
+    std::vector<int64_t> run_lrow(runs.size(), 0);
+    for (size_t k = 1; k < runs.size(); ++k) run_lrow[k] = run_lrow[k - 1] + runs[k - 1].second;
+    const int64_t npix = (int64_t)n_rows * W;
+    std::vector<int64_t> segs;  // (first double, doubles, masked, local offset)
     for (int s = 0; s < ns; ++s)
         for (int j = 0; j < 4; ++j) {
             if (!((plane_mask >> j) & 1)) continue;
             const int64_t pbase = (int64_t)(s * 4 + j) * Hf;
+            const int64_t lbase = (int64_t)(s * 4 + j) * npix;
             for (size_t k = 0; k < runs.size();) {
                 size_t e = k + 1;
                 if (regular_ok && runs[k].second == rlen)
@@ -1738,21 +1809,23 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
                            (int64_t)(runs[e].first + rlen - runs[k].first) * W <= MT_MERGE_DOUBLES)
                         ++e;
                 int64_t d0 = (pbase + runs[k].first) * W;
+                int64_t l0 = lbase + run_lrow[k] * W;
                 if (e > k + 1) {
-                    segs.insert(segs.end(), {d0, (int64_t)(runs[e - 1].first + rlen - runs[k].first) * W, 1});
+                    segs.insert(segs.end(), {d0, (int64_t)(runs[e - 1].first + rlen - runs[k].first) * W, 1, l0});
                 } else {
                     int64_t n = (int64_t)runs[k].second * W;
                     while (n > 0) {
                         const int64_t m = std::min<int64_t>(n, (int64_t)1 << 18);
-                        segs.insert(segs.end(), {d0, m, 0});
+                        segs.insert(segs.end(), {d0, m, 0, l0});
                         d0 += m;
+                        l0 += m;
                         n -= m;
                     }
                 }
                 k = e;
             }
         }
-    const int nseg = (int)(segs.size() / 3);
+    const int nseg = (int)(segs.size() / 4);
     *out = nullptr;
     if (nseg > MT_MAX_BANDS || nseg == 0) return SRT_OK;  // (the tabulated segments instead)
     std::vector<uint32_t> polys((size_t)nseg * rtmt::N, 0u);
@@ -1761,8 +1834,8 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
     for (int w = 0; w < nth; ++w)
         th.emplace_back([&, w] {
             for (int i = w; i < nseg; i += nth) {
-                if (segs[3 * i] == 0) continue;  // starts from the key
-                const std::vector<uint32_t> p = rtmt::xpow_mod((uint64_t)(2 * segs[3 * i] - 1));
+                if (segs[4 * i] == 0) continue;  // starts from the key
+                const std::vector<uint32_t> p = rtmt::xpow_mod((uint64_t)(2 * segs[4 * i] - 1));
                 std::copy(p.begin(), p.end(), polys.begin() + (size_t)i * rtmt::N);
             }
         });
@@ -1806,6 +1879,7 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     A.end_poly = end_poly;
     A.end_at = (int64_t)rtmt::end_jump(n_words);
     A.key_in_win = 1;
+    A.compact = 1;  // the shard's own layout (srt_render reads it by local pixel)
     A.y = mt_y_for(c, st, key);
     A.y_next = mt_ybuf(c, c->mt_cur ^ 1);
     hipLaunchKernelGGL(k_mt_jump, dim3(T.nseg + 1), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
@@ -2454,9 +2528,11 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         const int64_t g = c->frame_groups > 0 ? c->frame_groups : (want + ntiles - 1) / ntiles;
         F.groups = (int)std::max<int64_t>(1, std::min<int64_t>(g, batch));
     }
+    // fused paths (single-child scenes): by default when the frame's threads (sample groups
+    // included, pix_groups) fill two rounds of the resident threads
     F.fuse = !F.frame && c->fanout == 1 && c->chain_ok && pick_variant(c->mats).fused &&
              (c->fuse_primary > 0 ||
-              (c->fuse_primary < 0 && npix >= 2 * (int64_t)c->ncu * 4 * OCC * 64));
+              (c->fuse_primary < 0 && npix * pix_groups(c, npix, batch, true) >= fused_items(c)));
     if (!F.fuse && !F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
         c->hint_key[2] == batch) {
         for (int d = 1; d <= F.dcap; ++d)
@@ -2496,7 +2572,14 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         }
         if (!mt_bt[0] || !mt_bt[1]) mt_bt[0] = mt_bt[1] = nullptr;
     }
-    const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * W * Hf : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
+    // band mode stores a shard's jitter in its own layout [s][plane][its rows][W] (1/N of the frame's)
+    // when every pass generates in band mode (a pass whose generation ends inside the key window
+    // takes the tabulated segments and the frame's layout)
+    auto pass_words = [&](int ns, bool last) { return 2 * ((int64_t)ns * 4 * W * Hf + (last ? 4 * W * Hf : 0)); };
+    const bool jit_compact = mt_bt[0] && rtmt::end_jump(pass_words(a->spp - (F.npass - 1) * batch, true)) > 0 &&
+                             (F.npass == 1 || rtmt::end_jump(pass_words(batch, false)) > 0);
+    const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * (jit_compact ? npix : W * Hf)
+                                       : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
     const int64_t maxpix = sharded ? shard_max_rows(Hf, c->nranks, band, c->shard_snake) * W : 0;  // the gather's tile
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
     // for them (and reports their errors)
@@ -2660,21 +2743,15 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.fb = c->f->fb;
             P.fbx = (c->deterministic && c->fx_ok) ? c->f->fbx : nullptr;
             P.fb_first = (p == 0);  // the first pass's depth-0 kernel stores the framebuffer (no memset)
-            // samples per k_primary thread: all of the pass's (accumulated in registers) unless the
-            // frame has fewer pixels than a quarter of the resident wave slots, then fewer (pixel x
-            // sample-group items, framebuffer atomics on a zeroed framebuffer).  Measured on a
-            // 1/8 shard of ex1 1080p (261k pixels): 6 samples per thread 118 us, 1 sample 133 us, so
-            // only really small frames split.
-            P.spt = ns;
-            {
-                const int64_t want_items = (int64_t)c->max_blocks * 64;
-                while (P.spt > 1 && npix * ((ns + P.spt - 1) / P.spt) < want_items) P.spt = (P.spt + 1) / 2;
-                if (P.spt < ns && p == 0) {
-                    HIP_TRY(hipMemsetAsync(c->f->fb, 0, (size_t)3 * npix * 8, c->f->stream));
-                    if (c->deterministic && c->fx_ok)
-                        HIP_TRY(hipMemsetAsync(c->f->fbx, 0, (size_t)fx_words(npix) * 8, c->f->stream));
-                }
-            }
+            // sample groups per pixel (k_primary): one (all of the pass's samples in one thread, summed
+            // in registers) unless the frame has too few pixels to fill the GPU -- one GPU's shard of a
+            // multi-GPU frame -- then 2, 4, .. groups on lanes of the pixel's wave (their fixed-point
+            // sums are exact in any grouping: the image does not depend on it).  Enough means one
+            // round of the resident threads for the per-depth kernels (a 1/8 shard of ex1 1080p, 261k
+            // pixels: 6 samples per thread 118 us, 1 sample 133 us) and two for the fused paths, whose
+            // threads trace whole paths (long tails: a 1/8 shard on one group per pixel 0.35 ms, 1.3
+            // rounds, against 0.29 ms on the per-depth kernels)
+            P.pix_groups = pix_groups(c, npix, ns, F.fuse);
             P.npix = npix;
             P.cam = *cam;
             P.cam.xs = c->xs;
@@ -2715,8 +2792,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                     HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->jit_ready, 0));
                 }
                 P.jitter = c->f->jit;
-                P.jit_plane = W * Hf;
-                P.jit_global = 1;
+                P.jit_plane = band ? npix : W * Hf;
+                P.jit_global = band ? 0 : 1;
             } else if (a->jitter) {
                 const double* src = a->jitter + (int64_t)s0 * 4 * npix;
                 if (jit_dev) {
@@ -2768,8 +2845,15 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.cnt_out = c->f->counts + NSHARD;
             P.dcap = F.dcap;
             HIP_TRY(hipEventRecord(ev[0], c->f->stream));
-            hipLaunchKernelGGL(F.fuse ? V.fused : V.primary, dim3(grid_for(npix * ((ns + P.spt - 1) / P.spt), c->max_blocks)),
-                               dim3(BLOCK), lut_bytes(c), c->f->stream, P);
+            // a single-pass fused frame resolves its pixels in k_primary (no framebuffer)
+            P.fuse_resolve = F.fuse && F.npass == 1;
+            P.out_rgb = res_rgb;
+            P.out_u8 = res_u8;
+            P.spp_total = a->spp;
+            if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
+            hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
+                               dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
+                               lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
@@ -2809,8 +2893,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         }
         if (use_mt) c->mt_pos = mt_pos;
         uint32_t* hshadow = c->f->host + F.npass * F.pass_words;
-        // (a single-pass frame kernel has resolved its pixels: k_resolve only hands over the shadow count)
-        const bool fused = F.frame && F.npass == 1 && F.groups == 1;
+        // (a single-pass frame kernel or fused frame has resolved its pixels: k_resolve only hands over
+        // the counters and the shadow count)
+        const bool fused = F.npass == 1 && ((F.frame && F.groups == 1) || F.fuse);
         uint32_t* hlast = c->f->host + (F.npass - 1) * F.pass_words;
         if (c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
         hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,

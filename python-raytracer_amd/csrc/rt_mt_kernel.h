@@ -27,17 +27,19 @@ struct MtArgs {
     const uint32_t* end_poly;  // x^end_at mod phi: k_mt_jump's last block makes the final window (dump_dst)
     int64_t end_at;            // window position of that jump
     int32_t key_in_win;        // the key window is copied to win[0] by k_mt_jump (segment 0 reads it there)
-    int32_t pad_;
+    int32_t compact;           // band mode: doubles stored at the segment's local offset (bands[4 s + 3])
     // y: the MT_YBLOCKS x 624 raw words generated from the key window (k_mt_y, or the previous
     // frame's end block), read by every jump block instead of each block generating them itself
     const uint32_t* y;
     uint32_t* y_next;     // end block: the y of the final window (the next frame's key), or null
-    // band mode (a shard's rows): segment s covers bands[3 s + 1] doubles from double bands[3 s] of
-    // the call (runs of rows of one jitter plane), jumped to by tab[s] = x^(2 bands[3 s] - 1) mod
-    // phi (host-made per frame shape); its window is win[s + 1] (win[0]: the key).  bands[3 s + 2]
+    // band mode (a shard's rows): segment s covers bands[4 s + 1] doubles from double bands[4 s] of
+    // the call (runs of rows of one jitter plane), jumped to by tab[s] = x^(2 bands[4 s] - 1) mod
+    // phi (host-made per frame shape); its window is win[s + 1] (win[0]: the key).  bands[4 s + 2]
     // != 0: several runs merged, the segment generates through the other ranks' rows between them
-    // and stores double k only where k % band_period < band_len.  Null: the tabulated 2^19-word
-    // segments.
+    // and stores double k only where k % band_period < band_len.  With `compact` the doubles go to
+    // the shard's own layout -- [sample][plane][its rows][width], from out + bands[4 s + 3], a merged
+    // segment's band j of band_len doubles right after band j - 1 -- instead of the whole frame's
+    // (a shard stores 1/N of the frame's jitter).  Null: the tabulated 2^19-word segments.
     const int64_t* bands;
     int64_t band_len, band_period;
 };
@@ -109,6 +111,7 @@ struct MtSeg {
     int64_t ws;       // round-relative index of the segment's window
     int64_t lo;       // first output word
     int64_t dbase;    // double of pair 0
+    int64_t obase;    // where pair 0 is stored (out + obase; band mode compact: the local offset)
     int64_t gen_end;  // words to generate (exclusive)
     int64_t chain_at;
     int kend;         // pairs [0, kend) are stored (minus the planes outside plane_mask)
@@ -121,12 +124,13 @@ __device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
     MtSeg g;
     g.masked = false;
     if (A.bands) {
-        const int64_t d0 = A.bands[3 * s];
+        const int64_t d0 = A.bands[4 * s];
         g.ws = d0 == 0 ? 0 : 2 * d0 - 1;
         g.lo = 2 * d0 + A.pos;
         g.dbase = A.double_base + d0;
-        g.kend = (int)A.bands[3 * s + 1];
-        g.masked = A.bands[3 * s + 2] != 0;
+        g.obase = A.compact ? A.bands[4 * s + 3] : g.dbase;
+        g.kend = (int)A.bands[4 * s + 1];
+        g.masked = A.bands[4 * s + 2] != 0;
         g.gen_end = g.lo + 2 * (int64_t)g.kend;
         g.chain = g.dump = false;
         g.chain_at = 0;
@@ -138,6 +142,7 @@ __device__ __forceinline__ MtSeg mt_seg(const MtArgs& A, int s) {
     const int64_t hi = min((int64_t)(s + 1) * rtmt::L + A.pos, end);
     const int64_t npairs = hi > g.lo ? (hi - g.lo) / 2 : 0;
     g.dbase = A.double_base + (g.lo - A.pos) / 2;
+    g.obase = g.dbase;
     // a skipped draw (beyond n_out, or in a plane outside plane_mask) is only stepped over
     const int kmax = (int)max<int64_t>(0, min<int64_t>(npairs, A.n_out - g.dbase));
     g.kend = kmax;
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     const int t = threadIdx.x;
     if (blockIdx.x == 0)
         for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
-    if (!end_block && (band ? A.bands[3 * s] == 0 : mt_seg(A, s).idle())) return;
+    if (!end_block && (band ? A.bands[4 * s] == 0 : mt_seg(A, s).idle())) return;
     const uint32_t* poly = end_block ? A.end_poly : A.tab + (int64_t)(band ? s : s - 1) * rtmt::N;
     {
         const uint4* ys = reinterpret_cast<const uint4*>(A.y);
@@ -295,7 +300,8 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
     // block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it holds
     const int off0 = (int)(g.lo - g.ws);  // 1 .. 625 (s > 0) or pos (s == 0)
     const int c0 = -((off0 + 1) >> 1);    // pair index of block 0's first pair
-    double* outp = A.out + g.dbase;
+    double* outp = A.out + g.obase;
+    const bool cm = g.masked && A.compact;  // merged bands stored back to back
     // plane of pair k: pidx while k < kb, then pidx + 1 (a block's 312 pairs span at most two planes)
     int64_t pidx = 0, kb = INT64_MAX;
     if (A.plane > 0) {
@@ -345,7 +351,10 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
                 const int o = off0 + 2 * (c0 + t);  // in-block offset of the pair's first word: -1 .. 622
                 const uint32_t x0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
                 const uint32_t x1 = cur[o + 1];
-                outp[k] = rtmt::to_double(rtmt::temper(x0), rtmt::temper(x1));
+                const int64_t ko = cm ? (int64_t)((uint32_t)k / (uint32_t)A.band_period) * A.band_len +
+                                            (uint32_t)k % (uint32_t)A.band_period
+                                      : (int64_t)k;
+                outp[ko] = rtmt::to_double(rtmt::temper(x0), rtmt::temper(x1));
             }
         }
         if (g.chain || g.dump) {

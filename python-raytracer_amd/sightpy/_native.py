@@ -27,7 +27,7 @@ CF_SHADOW, CF_MC, CF_UV_CROSS = 1, 2, 4
 MF_ROUGH, MF_LIGHTMAP, MF_NOISE = 1, 2, 4
 LIGHT_DIRECTIONAL, LIGHT_POINT = 0, 1
 
-ERR_ARG, ERR_HIP, ERR_NOSCENE, ERR_MEMORY, ERR_INDEX, ERR_DEPTH = -1, -2, -3, -4, -5, -6
+ERR_ARG, ERR_HIP, ERR_NOSCENE, ERR_MEMORY, ERR_INDEX, ERR_DEPTH, ERR_NAME = -1, -2, -3, -4, -5, -6, -7
 
 COLLIDER_DTYPE = np.dtype(
     [
@@ -288,6 +288,8 @@ def check(lib, rc):
     msg = lib.srt_last_error().decode(errors="replace")
     if rc == ERR_INDEX:
         raise IndexError(msg)
+    if rc == ERR_NAME:
+        raise NameError(msg)
     raise SrtError(rc, msg)
 
 

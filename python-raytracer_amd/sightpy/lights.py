@@ -1,9 +1,11 @@
 """Lights (reference `sightpy/lights.py:6-52`).  Lights only affect Glossy materials.
 
 `DirectionalLight` is lowered to the device light table.  The reference `PointLight.get_L`
-references undefined names (lights.py:30-31) and raises NameError whenever a Glossy surface is
-shaded; here a point light is evaluated with its evident intent (L = (pos - P)/|pos - P|,
-irradiance = color * NdotL / dist^2 * 100) -- parity unpinned, no reference output exists.
+references undefined names (lights.py:30-31), so rendering a scene with a point light raises
+NameError as soon as a Glossy surface is shaded (glossy.py:38 calls get_L for every light).  Here
+the point light is lowered as a record and the device raises the same way: a Glossy hit under a
+point light sets an error bit and the render fails with SRT_ERR_NAME -> NameError.  Scenes whose
+rays never hit a Glossy surface render as in the reference (the light is never consulted).
 """
 import numpy as np
 
@@ -19,6 +21,10 @@ class Light:
 
 
 class PointLight(Light):
+    def get_L(self):
+        # lights.py:30-31: `(self.pos - M) * (1.0 / (dist_light))` with M, dist_light undefined
+        raise NameError("name 'M' is not defined")
+
     def get_distance(self, M):
         return np.sqrt((self.pos - M).dot(self.pos - M))
 

@@ -343,6 +343,79 @@ def test_gpu_fixed_point_sums_near_wrap_fall_back_to_f64_sums():
     np.testing.assert_allclose(out.rgb, rgb_o, rtol=RTOL, atol=ATOL)
 
 
+def _bright_light_example1(W, H, depth, color):
+    """example1 with a second DirectionalLight of the given colour: a Glossy-only scene (the
+    glossy+sky kernel variant, which has the fused paths) whose reflected terms can leave the
+    fixed-point range."""
+    from sightpy import rgb, vec3
+
+    sc = scenes.example1(W, H, depth)
+    sc.add_DirectionalLight(Ldir=vec3(-0.3, 0.8, -0.2), color=rgb(color, color, color))
+    return sc
+
+
+@pytest.mark.parametrize("color", [1e6, 3e4], ids=["term_beyond_2^17", "sum_past_magnitude_limit"])
+def test_gpu_fused_path_leaves_fixed_point_range_and_falls_back(color):
+    """The fused paths (every depth in k_primary) with terms beyond the fixed-point range: each
+    term is checked as fb_add checks it (|term| < 2^17, else left out of the sums and flagged
+    through the independent magnitude), the frame is rendered again with every depth summed in
+    the pixel's thread in f64, and matches the oracle."""
+    B = _backend()
+    sc = _bright_light_example1(64, 48, 4, color)
+    np.random.seed(11)
+    jit = sc.camera.draw_jitter(3)
+    _set_option("fuse_primary", 1)
+    try:
+        out = B.render_scene(sc, 3, jitter=jit, seed=1)
+        again = B.render_scene(sc, 3, jitter=jit, seed=1)  # (fixed-point sums now off for this scene)
+    finally:
+        _set_option("fuse_primary", -1)
+    assert out.stats["kernel_path"] == "fused" and again.stats["kernel_path"] == "fused"
+    assert out.stats["retries"] >= 1
+    rgb_o, ids, counts = O.render_linear(sc, jit)
+    np.testing.assert_allclose(out.rgb, rgb_o, rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(again.rgb, rgb_o, rtol=RTOL, atol=ATOL)
+    assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+
+
+def test_gpu_fused_path_without_fixed_point_sums_keeps_every_depth():
+    """Option deterministic=0 (f64 sums) on the fused paths: the deeper depths' colour goes into the
+    pixel's register sum, stored once with the depth-0 colour (an atomic add into the
+    framebuffer there was overwritten by the single-pass store, dropping the reflections)."""
+    B = _backend()
+    sc = scenes.example1(160, 120, 5)
+    np.random.seed(12)
+    jit = sc.camera.draw_jitter(2)
+    _set_option("fuse_primary", 1)
+    _set_option("deterministic", 0)
+    try:
+        out = B.render_scene(sc, 2, jitter=jit, seed=1)
+    finally:
+        _set_option("deterministic", 1)
+        _set_option("fuse_primary", -1)
+    assert out.stats["kernel_path"] == "fused"
+    rgb_o, ids, counts = O.render_linear(sc, jit)
+    np.testing.assert_allclose(out.rgb, rgb_o, rtol=RTOL, atol=ATOL)
+
+
+def test_gpu_point_light_raises_name_error_like_reference():
+    """PointLight.get_L reads undefined names (reference lights.py:30-31): the reference's render
+    raises NameError at the first Glossy hit.  So does this one; a scene whose rays never reach a
+    Glossy surface never consults the light and renders."""
+    from sightpy import rgb, vec3
+
+    sc = scenes.example1(32, 24, 2)
+    sc.add_PointLight(pos=vec3(0.0, 2.0, -3.0), color=rgb(1.0, 1.0, 1.0))
+    np.random.seed(0)
+    with pytest.raises(NameError):
+        sc.render(samples_per_pixel=1)
+    cb = scenes.cornell(16, 16)  # Diffuse / Emissive / Refractive only
+    cb.add_PointLight(pos=vec3(0.0, 0.2, 0.0), color=rgb(1.0, 1.0, 1.0))
+    np.random.seed(0)
+    img = cb.render(samples_per_pixel=1)
+    assert np.asarray(img).shape == (16, 16, 3)
+
+
 def test_gpu_group_render_retries_a_frame_on_every_context():
     """srt_render_group (Scene.render over $SIGHTPY_DEVICES) renders a frame that left the
     fixed-point range again on every context, as the single-GPU path does, instead of failing."""

@@ -49,16 +49,17 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> key(rtmt::N);
     uint32_t s = 5489u;
     for (int i = 0; i < rtmt::N; ++i) key[i] = s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
-    std::vector<int64_t> bands(3 * nb);
+    std::vector<int64_t> bands(4 * nb);
     std::vector<uint32_t> polys((size_t)nb * rtmt::N);
     for (int b = 0; b < nb; ++b) {
-        bands[3 * b] = (int64_t)(b + 1) * 8 * band;  // every 8th band
-        bands[3 * b + 1] = band;
-        bands[3 * b + 2] = 0;
-        std::vector<uint32_t> p = rtmt::xpow_mod((uint64_t)(2 * bands[3 * b] - 1));
+        bands[4 * b] = (int64_t)(b + 1) * 8 * band;  // every 8th band
+        bands[4 * b + 1] = band;
+        bands[4 * b + 2] = 0;
+        bands[4 * b + 3] = bands[4 * b];  // (stored in the frame's layout: compact = 0)
+        std::vector<uint32_t> p = rtmt::xpow_mod((uint64_t)(2 * bands[4 * b] - 1));
         std::copy(p.begin(), p.end(), polys.begin() + (size_t)b * rtmt::N);
     }
-    const int64_t n_words = 2 * (bands[3 * nb - 3] + band) + 4000;
+    const int64_t n_words = 2 * (bands[4 * nb - 4] + band) + 4000;
     std::vector<uint32_t> endp = rtmt::xpow_mod(rtmt::end_jump(n_words));
     uint32_t *dkey, *dy, *dyn, *dwin, *dpoly, *dend, *ddump;
     int64_t* dbands;
