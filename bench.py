@@ -9,10 +9,14 @@ memory:
   * every sample traced through every depth, the sRGB resolve;
   * the uint8 image and the linear RGB (f64) copied to pinned host memory.
 Frames are pipelined (each step queues its frame and returns; the timed region ends when all K
-frames are in host memory).  With N GPUs (one process per GPU, `torch.distributed.run` launches
-them; no torch is imported) the library splits each frame into 8-row bands dealt round-robin
-(SRT_RENDER_SHARDED), every rank draws the same stream and reads its rows, and the uint8 and
-linear-RGB tiles are gathered to rank 0 over RCCL (xGMI); the frame is fixed, so scaling is strong.
+frames are in host memory).  With N GPUs the library splits each frame into row bands dealt
+round-robin (SRT_RENDER_SHARDED), every rank draws the same stream and reads its rows, the uint8
+tiles are gathered to rank 0 over RCCL (xGMI) and every rank writes its rows of the linear RGB into
+the host frame over its own PCIe link; the frame is fixed, so scaling is strong.  Two launches, no
+torch imported in either: one process per GPU (WORLD_SIZE set by a launcher such as the driver's
+`torch.distributed.run`; the ranks meet through the library's srt_comm_init), or -- `--gpus N` with no
+launcher -- this one process driving all N GPUs through the library's group (srt_comm_init_all +
+pipelined srt_render_group).
 
 Secondary figures in the same line: `frame_latency_ms` (one synchronous frame), `device_resident`
 (jitter pre-resident in HBM and outputs left in HBM: the round-1 headline), the roofline of the
@@ -59,14 +63,15 @@ RAY_BYTES = 84  # one queued ray record (rt_kernels.hip Queue): O, D, throughput
 BYTES_MODEL = {
     "primary": "jitter read (2 f64 per sample, 4 for a thin lens) + the depth-1 children written to the queue "
                "(84 B each) + the framebuffer store (3 f64 per pixel); depth-0 rays live in registers",
-    "fused": "jitter read (2 f64 per sample, 4 for a thin lens) + the framebuffer store (3 f64) and the deeper "
-             "depths' fixed-point sums (3 x 8 B + 4 B) per pixel; every ray of every depth lives in registers",
+    "fused": "jitter read (2 f64 per sample, 4 for a thin lens) + per pixel the resolved linear RGB (3 f64) and "
+             "uint8 (3 B) of a single-pass frame (the fused resolve), else its fixed-point sums (3 x 8 B + 4 B) "
+             "read and written; every ray of every depth lives in registers",
     "frame": "jitter read + every secondary ray written to and read back from its wave's ring (2 x 84 B) + the "
              "fused resolve's uint8 and linear-RGB stores (27 B per pixel)",
 }
 
 
-def kernel_bytes_model(stats, spp, npix, lens):
+def kernel_bytes_model(stats, spp, npix, lens, npass=1):
     """Algorithmic HBM bytes of one launch of the dominant kernel, from what it moves (DESIGN.md §3);
     texture and scene-table reads are cache-resident and not counted (BYTES_MODEL)."""
     planes = 4 if lens else 2
@@ -74,7 +79,7 @@ def kernel_bytes_model(stats, spp, npix, lens):
     if stats["kernel_path"] == "frame":
         return spp * npix * planes * 8 + sum(rpd[1:]) * 2 * RAY_BYTES + npix * 27
     if stats["kernel_path"] == "fused":
-        return spp * npix * planes * 8 + npix * (24 + 28)
+        return spp * npix * planes * 8 + npix * (27 if npass == 1 else 2 * 28)
     children = rpd[1] if len(rpd) > 1 else 0
     return spp * npix * planes * 8 + children * RAY_BYTES + npix * 24
 
@@ -144,11 +149,12 @@ def cpu_baseline(builder, W, H, depth, spp, frame_rays, tile_of=0, budget_s=15.0
     GPU-counted frame's rays at the measured rate."""
     import multiprocessing as mp
     import scenes
-    from sightpy._shard import shard_rows
+    from sightpy._shard import scene_fanout, shard_rows
 
     sc = getattr(scenes, builder)(W, H, depth)
     np.random.seed(0)
-    rows = shard_rows(H, tile_of, 0) if tile_of > 1 else None
+    # (rank 0's rows as the library deals them: 2-row bands for a Diffuse fan-out scene)
+    rows = shard_rows(H, tile_of, 0, fanout=scene_fanout(sc)) if tile_of > 1 else None
     npx = (len(rows) if rows is not None else H) * W
     try:
         avail = len(os.sched_getaffinity(0))
@@ -331,12 +337,16 @@ def visible_gpus():
     return n
 
 
+GROUP = "group"  # launch_plan: one process drives the N GPUs through the library's own group
+
+
 def launch_plan(gpus, env, n_visible, argv):
-    """How `bench.py --gpus N` runs: None = in this process (N == WORLD_SIZE, one rank per GPU, as the
-    driver launches it through torch.distributed.run); a command = start N ranks through
-    torch.distributed.run as a child process (WORLD_SIZE unset, N > 1).  Refuses (SystemExit, rc 2)
-    rather than measure fewer GPUs than asked: fewer than N GPUs visible, or a launcher whose
-    WORLD_SIZE differs from N."""
+    """How `bench.py --gpus N` runs: None = one rank in this process (N == 1, or N == WORLD_SIZE: one
+    process per GPU, as the driver launches it through torch.distributed.run); GROUP = this process
+    drives all N GPUs itself (WORLD_SIZE unset, N > 1) through the library's torch-free multi-GPU path
+    -- srt_comm_init_all (one RCCL communicator over the N devices) and pipelined srt_render_group
+    frames.  Refuses (SystemExit, rc 2) rather than measure fewer GPUs than asked: fewer than N GPUs
+    visible, or a launcher whose WORLD_SIZE differs from N."""
     if gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     world = env.get("WORLD_SIZE")
@@ -349,13 +359,123 @@ def launch_plan(gpus, env, n_visible, argv):
     if n_visible < gpus:
         raise SystemExit("bench.py: --gpus %d but only %d GPU(s) visible; refusing to report an N=%d line "
                          "measured on fewer GPUs" % (gpus, n_visible, gpus))
-    import socket
+    return GROUP
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
-            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + list(argv)
+
+def run_group(args, gpus):
+    """`bench.py --gpus N` in one process (no launcher, no torch): contexts on devices 0..N-1 with one
+    RCCL communicator (srt_comm_init_all), every frame a pipelined srt_render_group -- each GPU renders
+    its row bands (SRT_RENDER_SHARDED), the uint8 tiles are gathered to device 0 over RCCL (xGMI) and
+    every GPU writes its rows of the linear RGB into the pinned host frame over its own PCIe link
+    (SRT_RENDER_RGB_ROWS).  Returns the JSON record (without the CPU baseline)."""
+    import scenes
+    from sightpy import _backend as B, _native as N
+    from sightpy._shard import SHARD_SNAKE, band_height, scene_fanout, shard_kmax
+
+    builder, W, H, depth, spp, label = CONFIGS[args.config]
+    if args.spp:
+        spp = args.spp
+    if args.size:
+        W, H = (int(v) for v in args.size.lower().split("x"))
+    sc = getattr(scenes, builder)(W, H, depth)
+    lib = B.library()
+    devs = (ctypes.c_int * gpus)(*range(gpus))
+    ctxs = (ctypes.c_void_p * gpus)()
+    N.check(lib, lib.srt_comm_init_all(gpus, devs, ctxs))
+    ctx = [ctypes.c_void_p(ctxs[q]) for q in range(gpus)]
+    nr, rk = ctypes.c_int(0), ctypes.c_int(0)
+    N.check(lib, lib.srt_comm_rank(ctx[0], ctypes.byref(nr), ctypes.byref(rk)))
+    if nr.value != gpus:
+        raise SystemExit("bench.py: the library's group has %d ranks, asked for %d" % (nr.value, gpus))
+    for c in ctx:
+        N.check(lib, lib.srt_set_option(c, b"pipeline", 1))
+        if args.shard_bands:
+            N.check(lib, lib.srt_set_option(c, b"shard_bands", args.shard_bands))
+        if args.shard_snake >= 0:
+            N.check(lib, lib.srt_set_option(c, b"shard_snake", args.shard_snake))
+        for kv in args.option:
+            k, v = kv.split("=")
+            N.check(lib, lib.srt_set_option(c, k.encode(), int(v)))
+        B.upload(sc, ctx=c)
+    cd = B.camera_desc(sc.camera)
+    NOUT = 3
+    outs = []
+    for _ in range(NOUT):
+        pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(lib, lib.srt_host_alloc(ctx[0], 3 * W * H, ctypes.byref(pu)))
+        N.check(lib, lib.srt_host_alloc(ctx[0], 3 * W * H * 8, ctypes.byref(pr)))
+        outs.append((pu, pr))
+    np.random.seed(0)
+    mt = N.MtState.from_numpy()
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, H, 0
+    a.rows, a.jitter, a.out_hit_id = None, None, None
+    a.mt = ctypes.pointer(mt) if args.rng == "mt" else None
+    a.seed = 12345
+    frame = {"k": 0}
+
+    def step(async_ok=True, st=None):
+        u8, rgb = outs[frame["k"] % NOUT]
+        frame["k"] += 1
+        a.out_srgb8, a.out_rgb = u8, rgb
+        a.flags = (N.RENDER_ASYNC | N.RENDER_RGB_ROWS) if async_ok else 0
+        N.check(lib, lib.srt_render_group(ctxs, gpus, ctypes.byref(cd), ctypes.byref(a),
+                                          ctypes.byref(st) if st is not None else None))
+
+    for w in range(args.warmup):
+        step(async_ok=w > 0)  # the first frame synchronously (sizes queues and rings on every GPU)
+    N.check(lib, lib.srt_render_group_finish(ctxs, gpus, None))
+    for c in ctx:
+        N.check(lib, lib.srt_synchronize(c))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(async_ok=not args.sync)
+    last = N.Stats()
+    N.check(lib, lib.srt_render_group_finish(ctxs, gpus, ctypes.byref(last)))  # every GPU's frames done
+    for c in ctx:
+        N.check(lib, lib.srt_synchronize(c))
+    el = time.perf_counter() - t0
+    last = last.as_dict()
+    ms_step = el / args.steps * 1e3
+    rec = {
+        "metric": "Mrays/sec (primary+secondary) + frame ms at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
+        else "Mrays/sec (primary+secondary) + frame ms",
+        "value": round(last["total_rays"] * args.steps / el / 1e6, 3),
+        "unit": "Mrays/s", "n_gpus": gpus, "nranks": nr.value, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: %s; jitter = the reference's numpy stream (seed 0, continued frame to frame) %s"
+                % (label, "generated on every GPU inside each step" if args.rng == "mt" else "replaced by device Philox"),
+        "config": {"workload": label, "width": W, "height": H, "max_ray_depth": depth, "spp": spp,
+                   "rays_per_frame": int(last["total_rays"]), "rays_per_depth": last["rays_per_depth"],
+                   "shadow_rays": last["shadow_rays"], "kernel_path_rank0": last["kernel_path"],
+                   "parallelism": "row-band shards x%d in one process (srt_comm_init_all + pipelined "
+                                  "srt_render_group, no torch): uint8 tiles gathered to GPU 0 over RCCL (xGMI); every "
+                                  "GPU writes its rows of the linear RGB into the pinned host frame over its own PCIe "
+                                  "link" % gpus,
+                   "frame": "render_group() entry (scene resident on every GPU) -> jitter stream on every GPU -> all "
+                            "samples and depths -> sRGB resolve -> gather -> uint8 + linear RGB (f64) in pinned host "
+                            "memory; frames pipelined",
+                   "frame_ms": round(ms_step, 4),
+                   "row_bands": {"kmax": shard_kmax(H, gpus, args.shard_bands, scene_fanout(sc)),
+                                 "snake": args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE,
+                                 "band_height": band_height(H, gpus, shard_kmax(H, gpus, args.shard_bands,
+                                                                                scene_fanout(sc)),
+                                                            args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE)}},
+    }
+    if not args.no_secondary:
+        lat = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            step(async_ok=False, st=N.Stats())
+            lat.append((time.perf_counter() - t1) * 1e3)
+        rec["config"]["frame_latency_ms"] = round(float(np.median(lat)), 4)
+    for pu, pr in outs:
+        lib.srt_host_free(ctx[0], pu)
+        lib.srt_host_free(ctx[0], pr)
+    for c in ctx:
+        lib.srt_destroy(c)
+    return rec
 
 
 def main():
@@ -387,12 +507,12 @@ def main():
                     help="band dealing order, 0 round-robin / 1 snake (library option shard_snake; default SHARD_SNAKE)")
     args = ap.parse_args()
 
-    cmd = launch_plan(args.gpus, os.environ, visible_gpus() if "WORLD_SIZE" not in os.environ and args.gpus > 1
-                      else args.gpus, sys.argv[1:])
-    if cmd is not None:
-        # one process per GPU: the ranks are children of torch.distributed.run (nothing here has
-        # touched the GPU); rank 0 prints the line
-        sys.exit(subprocess.run(cmd).returncode)
+    plan = launch_plan(args.gpus, os.environ, visible_gpus() if "WORLD_SIZE" not in os.environ and args.gpus > 1
+                       else args.gpus, sys.argv[1:])
+    if plan == GROUP:
+        # this process drives the N GPUs (the library's RCCL group); no CPU baseline at N > 1
+        print(json.dumps(run_group(args, args.gpus)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -627,7 +747,7 @@ def main():
             npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0, kmax, snake)) * W
             st_pass = dict(st0[0])
             st_pass["rays_per_depth"] = [r / npass for r in st0[0]["rays_per_depth"]]
-            model = kernel_bytes_model(st_pass, spp / npass, npix_rank, sc.camera.lens_radius != 0.0)
+            model = kernel_bytes_model(st_pass, spp / npass, npix_rank, sc.camera.lens_radius != 0.0, npass)
             roof = roofline(kname + (" (fused paths)" if path == "fused" else ""), kms, model, path, krec, src)
             if npass > 1:
                 roof["passes_per_frame"] = npass

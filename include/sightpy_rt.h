@@ -23,6 +23,7 @@
  *                             (sphere.py:17,54-64, plane.py:34,98-105, cuboid.py:29,142-187,
  *                              triangle.py:85, skybox.py:29)
  *   srt_texture_lookup     <- image.get_color(hit)     sightpy/textures/texture.py:32-39
+ *   srt_material_normal    <- Material.get_Normal(hit) sightpy/materials/material.py:18-36
  *   srt_primary_rays       <- Camera.get_ray(n)       sightpy/camera.py:51-85
  *   srt_upload_scene       <- (scene lowering; the reference deep-copies the Scene per task,
  *                              scene.py:85)
@@ -323,6 +324,15 @@ int srt_collider_surface(srt_ctx* ctx, const srt_collider* collider, const doubl
  * fail with SRT_ERR_INDEX as numpy indexing raises. */
 int srt_texture_lookup(srt_ctx* ctx, const srt_texture* tex, const uint8_t* texels, int64_t texel_bytes,
                        const double* uv, int64_t n, double* rgb);
+/* Material.get_Normal(hit) at points P [3][n] on the collider with orientations orient [n]: the
+ * collider's normal, or -- normalmap not NULL, a record over `texels` (texel_bytes bytes) whose
+ * table maps a byte b to b/256 -- the map's texel at the primitive's uv taken through the
+ * collider's inverse_basis_matrix and normalised (Plane and Cuboid colliders: the reference's other
+ * colliders have no inverse_basis_matrix), times the orientation; N [3][n].
+ * Replaces sightpy/materials/material.py:18-36. */
+int srt_material_normal(srt_ctx* ctx, const srt_collider* collider, const srt_texture* normalmap,
+                        const uint8_t* texels, int64_t texel_bytes, const double* P, const double* orient,
+                        int64_t n, double* N);
 int srt_primary_rays(srt_ctx* ctx, const srt_camera* cam, const double* jitter /* [4][n] */,
                      double* origin /* [3][n] */, double* dir /* [3][n] */);
 /* numpy's legacy global-RNG stream on the device: writes the n_out doubles that
@@ -347,8 +357,15 @@ int srt_comm_init(srt_ctx* ctx, int nranks, int rank, const uint8_t* id);
 int srt_comm_init_all(int ndev, const int* devs, srt_ctx** ctxs /* [ndev], out */);
 int srt_comm_rank(srt_ctx* ctx, int* nranks, int* rank);
 /* frame of srt_render on every context of an srt_comm_init_all group; args of rank 0 (its outputs
- * receive the frame), stats of rank 0 plus total_rays / rays_per_depth / shadow_rays summed */
+ * receive the frame), stats of rank 0 plus total_rays / rays_per_depth / shadow_rays summed.
+ * args->flags may hold SRT_RENDER_ASYNC (queue the frame on every context, gather posted, return at
+ * once; outputs in pinned host memory from srt_host_alloc; `stats` not written; finish with
+ * srt_render_group_finish) and SRT_RENDER_RGB_ROWS (with ASYNC: every context writes its rows of the
+ * linear RGB into out_rgb over its own PCIe link instead of the RCCL gather to rank 0). */
 int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);
+/* wait for the group's asynchronous frames: errors of every context, the last frame's stats summed as
+ * srt_render_group returns them */
+int srt_render_group_finish(srt_ctx** ctxs, int n, srt_stats* stats);
 /* collectives over the communicator for callers' bookkeeping (host values, blocking):
  * op 0 = sum, 1 = max; n doubles */
 int srt_comm_allreduce(srt_ctx* ctx, double* vals, int n, int op);

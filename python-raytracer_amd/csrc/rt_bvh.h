@@ -7,10 +7,13 @@
 // (smallest distance, then lowest collider index, ties recorded), so results equal the linear loop
 // over `scene.collider_list` (ray.py:124-132).
 //
-// Build: binned SAH (16 bins on the longest centroid axis), leaves of at most 4 triangles, depth
-// capped below the traversal stack.  Boxes are the triangles' vertex boxes inflated by
-// 1e-9 * (1 + max |coordinate|): the reference intersects the plane through the centroid and tests
-// edge half-spaces with >= 0, so a hit point may sit a few ulps outside the vertex box.
+// Build: a binary BVH by binned SAH (16 bins on the longest centroid axis), leaves of at most 4
+// triangles, depth capped at BVH_MAX_DEPTH; then collapsed into 4-wide nodes (rt_device.h BvhNode):
+// a node's slots start as its two children, and the slot of largest surface area that is an inner
+// node is replaced by its two children while fewer than four slots are taken.  Boxes are the
+// triangles' vertex boxes inflated by 1e-9 * (1 + max |coordinate|) -- the reference intersects the
+// plane through the centroid and tests edge half-spaces with >= 0, so a hit point may sit a few ulps
+// outside the vertex box -- then rounded outward to float.
 #pragma once
 
 #include <algorithm>
@@ -23,7 +26,8 @@ namespace rt {
 
 constexpr int BVH_MIN_TRIANGLES = 8;  // fewer triangles stay in the linear collider loop
 constexpr int BVH_LEAF = 4;
-constexpr int BVH_MAX_DEPTH = BVH_STACK - 4;
+constexpr int BVH_MAX_DEPTH = 30;  // binary levels (so at most 30 4-wide levels: 91 stack entries < BVH_STACK)
+static_assert(3 * BVH_MAX_DEPTH + 1 <= BVH_STACK, "traversal stack holds the deepest path");
 
 struct BvhBuild {
     std::vector<BvhNode> nodes;
@@ -32,6 +36,10 @@ struct BvhBuild {
 };
 
 namespace bvh_detail {
+struct BinNode {  // binary build node: count > 0 leaf of tri[first, first + count), else children first, first + 1
+    double lo[3], hi[3];
+    int32_t first, count;
+};
 struct Item {
     double lo[3], hi[3], c[3];
     int32_t col;
@@ -84,7 +92,8 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
     struct Task {
         int node, begin, end, depth;
     };
-    out.nodes.push_back(BvhNode{});
+    std::vector<BinNode> bin;
+    bin.push_back(BinNode{});
     std::vector<Task> tasks{{0, 0, (int)items.size(), 0}};
     while (!tasks.empty()) {
         const Task t = tasks.back();
@@ -95,7 +104,7 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
             grow(lo, hi, items[i].lo, items[i].hi);
             grow(clo, chi, items[i].c, items[i].c);
         }
-        BvhNode& nd = out.nodes[t.node];
+        BinNode& nd = bin[t.node];
         for (int k = 0; k < 3; ++k) {
             nd.lo[k] = lo[k];
             nd.hi[k] = hi[k];
@@ -165,13 +174,84 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
             for (int i = t.begin; i < t.end; ++i) out.tri.push_back(items[i].col);
             continue;
         }
-        const int left = (int)out.nodes.size();
+        const int left = (int)bin.size();
         nd.first = left;
         nd.count = 0;
-        out.nodes.push_back(BvhNode{});
-        out.nodes.push_back(BvhNode{});
+        bin.push_back(BinNode{});
+        bin.push_back(BinNode{});
         tasks.push_back({left, t.begin, mid, t.depth + 1});
         tasks.push_back({left + 1, mid, t.end, t.depth + 1});
+    }
+    // collapse into 4-wide nodes (node 0 = the root's children)
+    auto fdown = [](double x) {
+        float f = (float)x;
+        if ((double)f > x) f = std::nextafter(f, -INFINITY);
+        return f;
+    };
+    auto fup = [](double x) {
+        float f = (float)x;
+        if ((double)f < x) f = std::nextafter(f, INFINITY);
+        return f;
+    };
+    if (bin[0].count > 0) {  // a single leaf (not reached: BVH_MIN_TRIANGLES > BVH_LEAF)
+        bin.push_back(bin[0]);
+        bin[0].first = (int32_t)bin.size() - 1;
+        bin[0].count = 0;
+        bin.push_back(BinNode{});  // an empty box: never hit
+        for (int k = 0; k < 3; ++k) {
+            bin.back().lo[k] = INFINITY;
+            bin.back().hi[k] = -INFINITY;
+        }
+        bin.back().count = 0;
+        bin.back().first = -1;
+    }
+    std::vector<std::pair<int, int>> work{{0, 0}};  // (binary inner node, 4-wide node)
+    out.nodes.push_back(BvhNode{});
+    while (!work.empty()) {
+        const auto [bn, wn] = work.back();
+        work.pop_back();
+        std::vector<int> slots{bin[bn].first, bin[bn].first + 1};
+        while (slots.size() < 4) {
+            int pick = -1;
+            double pa = -1.0;
+            for (size_t k = 0; k < slots.size(); ++k) {
+                const BinNode& c = bin[slots[k]];
+                if (c.count > 0 || c.first < 0) continue;
+                const double a = area(c.lo, c.hi);
+                if (a > pa) { pa = a; pick = (int)k; }
+            }
+            if (pick < 0) break;
+            const int f = bin[slots[pick]].first;
+            slots[pick] = f;
+            slots.insert(slots.begin() + pick + 1, f + 1);
+        }
+        BvhNode nd4{};
+        for (int k = 0; k < 4; ++k) {
+            if (k >= (int)slots.size() || bin[slots[k]].first < 0) {
+                nd4.child[k] = BVH_EMPTY;
+                nd4.count[k] = 0;
+                for (int a = 0; a < 3; ++a) {
+                    nd4.lo[a][k] = INFINITY;
+                    nd4.hi[a][k] = -INFINITY;
+                }
+                continue;
+            }
+            const BinNode& c = bin[slots[k]];
+            for (int a = 0; a < 3; ++a) {
+                nd4.lo[a][k] = fdown(c.lo[a]);
+                nd4.hi[a][k] = fup(c.hi[a]);
+            }
+            if (c.count > 0) {
+                nd4.child[k] = -(c.first + 1);
+                nd4.count[k] = c.count;
+            } else {
+                nd4.child[k] = (int32_t)out.nodes.size();
+                nd4.count[k] = 0;
+                work.push_back({slots[k], (int)out.nodes.size()});
+                out.nodes.push_back(BvhNode{});
+            }
+        }
+        out.nodes[wn] = nd4;
     }
 }
 

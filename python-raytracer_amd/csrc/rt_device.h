@@ -241,17 +241,32 @@ struct SceneView {
 // the host builds SceneView/TraceParams and the device reads them: the layout must agree
 static_assert(sizeof(SceneView) == 176 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
 
-// BVH node (56 B): box [lo, hi] (inflated so that rounding never excludes a triangle's hit point);
-// count > 0: leaf of bvh_tri[first, first + count); count == 0: children at first and first + 1
+// BVH node, 4-wide (128 B: one traversal step loads one cache line and tests four boxes): child k's
+// box [lo[.][k], hi[.][k]] in float, rounded outward from the build's f64 boxes (which are inflated so
+// that rounding never excludes a triangle's hit point), so the f64 slab test on the float bounds is
+// conservative; child[k] >= 0: inner node; child[k] < 0 (and != BVH_EMPTY): leaf of the triangles
+// bvh_tri[-child[k] - 1, .. + count[k]); BVH_EMPTY: no child in slot k
 struct BvhNode {
-    double lo[3], hi[3];
-    int32_t first, count;
+    float lo[3][4], hi[3][4];
+    int32_t child[4];
+    int32_t count[4];
 };
-constexpr int BVH_STACK = 64;
+static_assert(sizeof(BvhNode) == 128, "one 128-byte line per BVH node");
+constexpr int32_t BVH_EMPTY = (int32_t)0x80000000;
+constexpr int BVH_STACK = 96;  // (3 entries per 4-wide level at most: depth <= 30 levels)
+
+// The kernel's dynamic LDS: the texture tables [0, nlut_lds) staged by the trace kernels first
+// (rt_kernels.hip stage_luts), read directly (no pointer in the scene view, so the kernels' scene view
+// needs no per-block copy of their arguments)
+#if defined(__HIPCC__)
+extern __shared__ double rt_lds_dyn[];
+#endif
 
 // lut[b] of texture `tid` (LDS copy when staged)
 RT_HD double tex_lut(const SceneView& S, int tid, uint8_t b) {
-    if (tid < S.nlut_lds) return S.lut_lds[tid * 256 + b];
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (tid < S.nlut_lds) return rt_lds_dyn[tid * 256 + b];
+#endif
     return S.tex[tid].lut[b];
 }
 
@@ -456,13 +471,29 @@ RT_HD const RT_RO uint8_t* tex_uv(const SceneView& S, const RT_RO srt_texture& T
     int64_t col = py_mod(np_trunc((u * (double)T.idx_w) * T.repeat), T.idx_w);
     return texel_at(S, T, -m, col, err);
 }
+// The three bytes of a texel through the texture's table.  A 4-byte texel read from its first byte
+// (RGBX: srt_upload_scene stores 3-channel images that way, and RGBA images are) is one aligned
+// dword load instead of three byte loads; other layouts read the bytes.
+RT_HD d3 texel_rgb(const SceneView& S, const RT_RO srt_texture& T, int tid, const RT_RO uint8_t* px) {
+    uint32_t b0, b1, b2;
+    if (T.channels == 4 && T.channel0 == 0) {
+        const uint32_t w = *reinterpret_cast<const RT_RO uint32_t*>(px);
+        b0 = w & 0xFFu;
+        b1 = (w >> 8) & 0xFFu;
+        b2 = (w >> 16) & 0xFFu;
+    } else {
+        b0 = px[0];
+        b1 = px[1];
+        b2 = px[2];
+    }
+    return d3{tex_lut(S, tid, (uint8_t)b0), tex_lut(S, tid, (uint8_t)b1), tex_lut(S, tid, (uint8_t)b2)};
+}
 RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err) {
     const RT_RO srt_texture& T = S.tex[tid];
 #ifdef RT_ABL_TEX  // diagnostic build only: no gathers
     return d3{u * T.repeat, v, u + v};
 #endif
-    const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
-    return d3{tex_lut(S, tid, px[0]), tex_lut(S, tid, px[1]), tex_lut(S, tid, px[2])};
+    return texel_rgb(S, T, tid, tex_uv(S, T, u, v, err));
 }
 
 // Material.get_Normal (material.py:18-36): collider normal (or normal map) times orientation
@@ -472,10 +503,8 @@ RT_HD d3 shading_normal(const SceneView& S, const RT_RO srt_collider& c, const R
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
         const RT_RO srt_texture& T = S.tex[m.normalmap];
-        const RT_RO uint8_t* px = tex_uv(S, T, u, v, err);
-        const int nmt = m.normalmap;
-        d3 nm = d3{(tex_lut(S, nmt, px[0]) - 0.5) * 2.0, (tex_lut(S, nmt, px[1]) - 0.5) * 2.0,
-                   (tex_lut(S, nmt, px[2]) - 0.5) * 2.0};
+        const d3 t = texel_rgb(S, T, m.normalmap, tex_uv(S, T, u, v, err));
+        d3 nm = d3{(t.x - 0.5) * 2.0, (t.y - 0.5) * 2.0, (t.z - 0.5) * 2.0};
         const RT_RO double* ib = (c.type == SRT_PLANE) ? c.p + 16 : c.p + 30;
         return mul(normalize(matmul_rows(ib, nm)), orient);
     }
@@ -565,16 +594,18 @@ RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double
 // Nearest collider over the scene (ray.py:124-132): nearest = reduce(np.minimum, distances);
 // a collider is hit where nearest != FARAWAY and its distance == nearest.  Returns the first
 // such collider (-1 if none); `ties` reports that a later collider hit at the same distance.
-// Ray/box slab test: entry distance `tnear`; an axis whose slab product is NaN (an axis-parallel
-// ray exactly on a slab plane) constrains nothing (conservative).
-RT_HD bool box_hit(const RT_RO BvhNode& nd, d3 O, d3 inv, double& tnear) {
+// Ray/box slab test of child k of a 4-wide node (f64 arithmetic on the float bounds): entry
+// distance `tnear`; an axis whose slab product is NaN (an axis-parallel ray exactly on a slab plane)
+// constrains nothing (conservative).
+RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear) {
     double t0 = -INFINITY, t1 = INFINITY;
     const double o[3] = {O.x, O.y, O.z}, iv[3] = {inv.x, inv.y, inv.z};
-    for (int k = 0; k < 3; ++k) {
-        const double a = (nd.lo[k] - o[k]) * iv[k], b = (nd.hi[k] - o[k]) * iv[k];
-        if (a != a || b != b) continue;
-        t0 = fmax(t0, fmin(a, b));
-        t1 = fmin(t1, fmax(a, b));
+    for (int a = 0; a < 3; ++a) {
+        const double lo = (double)nd.lo[a][k], hi = (double)nd.hi[a][k];
+        const double p = (lo - o[a]) * iv[a], q = (hi - o[a]) * iv[a];
+        if (p != p || q != q) continue;
+        t0 = fmax(t0, fmin(p, q));
+        t1 = fmin(t1, fmax(p, q));
     }
     tnear = t0;
     return t0 <= t1 && t1 >= 0.0;
@@ -583,31 +614,54 @@ RT_HD bool box_hit(const RT_RO BvhNode& nd, d3 O, d3 inv, double& tnear) {
 // Nearest BVH triangle, merged into (best, id, bo, ties) with the reference's rule independent of
 // visiting order: the smallest distance wins, among equal distances the lowest collider index,
 // and `ties` records that another collider hit at that distance.  Boxes entered beyond `best` are
-// pruned (a box entered exactly at `best` is still visited: it may hold a tie).  Triangles never
-// return NaN (a NaN ray fails every comparison of triangle_hit and misses).
+// pruned (a box entered exactly at `best` is still visited: it may hold a tie); a node's leaves are
+// tested at once, its inner children pushed farthest first (the nearest is popped next) with their
+// entry distance, which prunes them again on pop.  Triangles never return NaN (a NaN ray fails every
+// comparison of triangle_hit and misses).
 RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
     const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
     int stack[BVH_STACK];
+    double stn[BVH_STACK];
     int sp = 0;
-    stack[sp++] = 0;
+    stack[sp] = 0;
+    stn[sp++] = -INFINITY;
     while (sp > 0) {
-        const RT_RO BvhNode& nd = S.bvh[stack[--sp]];
-        double tn;
-        if (!box_hit(nd, O, inv, tn) || tn > best) continue;
-        if (nd.count > 0) {
-            for (int k = nd.first; k < nd.first + nd.count; ++k) {
-                const int c = S.bvh_tri[k];
-                double o;
-                const double t = triangle_hit(S.col[c].p, O, D, o);
-                if (t < best) { best = t; id = c; bo = o; ties = false; }
-                else if (t == best && best != FARAWAY) {
-                    ties = true;
-                    if (c < id) { id = c; bo = o; }
+        --sp;
+        if (stn[sp] > best) continue;
+        const RT_RO BvhNode& nd = S.bvh[stack[sp]];
+        int in[4];
+        double it[4];
+        int ni = 0;
+        for (int k = 0; k < 4; ++k) {
+            const int32_t ch = nd.child[k];
+            double tn;
+            if (ch == BVH_EMPTY || !box4_hit(nd, k, O, inv, tn) || tn > best) continue;
+            if (ch < 0) {
+                for (int j = -ch - 1, e = -ch - 1 + nd.count[k]; j < e; ++j) {
+                    const int c = S.bvh_tri[j];
+                    double o;
+                    const double t = triangle_hit(S.col[c].p, O, D, o);
+                    if (t < best) { best = t; id = c; bo = o; ties = false; }
+                    else if (t == best && best != FARAWAY) {
+                        ties = true;
+                        if (c < id) { id = c; bo = o; }
+                    }
                 }
+            } else {
+                // insertion by entry distance, nearest last
+                int j = ni++;
+                while (j > 0 && it[j - 1] < tn) {
+                    in[j] = in[j - 1];
+                    it[j] = it[j - 1];
+                    --j;
+                }
+                in[j] = ch;
+                it[j] = tn;
             }
-        } else if (sp + 2 <= BVH_STACK) {
-            stack[sp++] = nd.first + 1;
-            stack[sp++] = nd.first;
+        }
+        for (int j = 0; j < ni && sp < BVH_STACK; ++j) {
+            stack[sp] = in[j];
+            stn[sp++] = it[j];
         }
     }
 }
@@ -620,19 +674,21 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
     stack[sp++] = 0;
     while (sp > 0) {
         const RT_RO BvhNode& nd = S.bvh[stack[--sp]];
-        double tn;
-        if (!box_hit(nd, O, inv, tn) || tn >= stop) continue;
-        if (nd.count > 0) {
-            for (int k = nd.first; k < nd.first + nd.count; ++k) {
-                const RT_RO srt_collider& cc = S.col[S.bvh_tri[k]];
-                if (!(cc.flags & SRT_CF_SHADOW)) continue;
-                double o;
-                const double t = triangle_hit(cc.p, O, L, o);
-                if (t < stop) return t;
+        for (int k = 0; k < 4; ++k) {
+            const int32_t ch = nd.child[k];
+            double tn;
+            if (ch == BVH_EMPTY || !box4_hit(nd, k, O, inv, tn) || tn >= stop) continue;
+            if (ch < 0) {
+                for (int j = -ch - 1, e = -ch - 1 + nd.count[k]; j < e; ++j) {
+                    const RT_RO srt_collider& cc = S.col[S.bvh_tri[j]];
+                    if (!(cc.flags & SRT_CF_SHADOW)) continue;
+                    double o;
+                    const double t = triangle_hit(cc.p, O, L, o);
+                    if (t < stop) return t;
+                }
+            } else if (sp < BVH_STACK) {
+                stack[sp++] = ch;
             }
-        } else if (sp + 2 <= BVH_STACK) {
-            stack[sp++] = nd.first + 1;
-            stack[sp++] = nd.first;
         }
     }
     return FARAWAY;
@@ -930,9 +986,7 @@ RT_HD void shade_thinfilm(const SceneView& S, const RT_RO srt_collider& c, int m
     } else {
         ti = (int64_t)m.p[0];
     }
-    const RT_RO uint8_t* px = texel_at(S, lut, li, ti, err);
-    const int lt = m.tex_aux0;
-    d3 F = d3{tex_lut(S, lt, px[0]), tex_lut(S, lt, px[1]), tex_lut(S, lt, px[2])};
+    d3 F = texel_rgb(S, lut, m.tex_aux0, texel_at(S, lut, li, ti, err));
     em.local(mul(ld3(S.ambient), F));
     uint32_t med = meta_medium(r.meta), dfl = meta_diffuse(r.meta);
     em.child(mkchild(add(P, mul(N, NUDGE)), reflect_dir(r.d, N), F, med, dfl, 1));
@@ -958,10 +1012,8 @@ RT_HD void shade_sky(const SceneView& S, const RT_RO srt_collider& c, int mi, co
     RT_ACC(11, tk1);
     if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP)) {
         const RT_RO srt_texture& L = S.tex[m.tex_aux0];
-        const RT_RO uint8_t* px = tex_uv(S, L, u, v, err);
-        const int lm = m.tex_aux0;
-        col = d3{col.x + m.p[0] * tex_lut(S, lm, px[0]), col.y + m.p[0] * tex_lut(S, lm, px[1]),
-                 col.z + m.p[0] * tex_lut(S, lm, px[2])};
+        const d3 lt = texel_rgb(S, L, m.tex_aux0, tex_uv(S, L, u, v, err));
+        col = d3{col.x + m.p[0] * lt.x, col.y + m.p[0] * lt.y, col.z + m.p[0] * lt.z};
     }
     em.local(col);
 }
@@ -1161,6 +1213,7 @@ RT_HD int64_t shard_band_height(int64_t H, int n, int kmax, int snake) {
     for (int k = kmax; k >= (kmax / 2 > 1 ? kmax / 2 : 1); --k) {
         int64_t h = (H + (int64_t)n * k - 1) / ((int64_t)n * k);
         if (h < 1) h = 1;
+        if ((H + h - 1) / h < n) continue;  // fewer bands than ranks: a rank would get no rows (then h = 1)
         const int64_t m = shard_max_rows(H, n, h, snake);
         if (m < best_rows) { best_rows = m; best_h = h; }
     }

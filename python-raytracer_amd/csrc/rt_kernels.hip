@@ -21,6 +21,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -307,6 +308,56 @@ struct PixAcc {
     }
 };
 
+// RT_PIX_LDS: the thread's PixAcc kept in LDS (its own slot; 28 B per thread after the texture
+// tables) instead of 7 VGPRs live across the whole trace: fixed-point terms are fire-and-forget
+// ds_add_u64 / ds_add_f32 (integer sums: exact in any order), f64 terms read-modify-write
+#ifdef RT_PIX_LDS
+struct PixAccLds {
+    RT_LDS unsigned long long* w;  // w[0], w[BLOCK], w[2 BLOCK]: this thread's three sums
+    RT_LDS float* mag;
+
+    __device__ __forceinline__ void zero() {
+        w[0] = 0ull;
+        w[BLOCK] = 0ull;
+        w[2 * BLOCK] = 0ull;
+        *mag = 0.0f;
+    }
+    __device__ __forceinline__ void add(bool fx, d3 t) {
+        if (fx) {
+            const double m = (fabs(t.x) + fabs(t.y)) + fabs(t.z);
+            if (m < FX_MAX) {
+                __hip_atomic_fetch_add(w, (unsigned long long)__double2ll_rn(t.x * FX_SCALE), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(w + BLOCK, (unsigned long long)__double2ll_rn(t.y * FX_SCALE), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(w + 2 * BLOCK, (unsigned long long)__double2ll_rn(t.z * FX_SCALE),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __hip_atomic_fetch_add(mag, (float)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            const double e[3] = {t.x, t.y, t.z};
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                w[k * BLOCK] = (unsigned long long)__double_as_longlong(
+                    __longlong_as_double((long long)w[k * BLOCK]) + e[k]);
+        }
+    }
+    __device__ __forceinline__ PixAcc load() const {
+        PixAcc a;
+        a.w[0] = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        a.w[1] = __hip_atomic_load(w + BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        a.w[2] = __hip_atomic_load(w + 2 * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        a.mag = __hip_atomic_load(mag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return a;
+    }
+};
+using PixAccT = PixAccLds;
+constexpr size_t PIX_LDS_BYTES = (size_t)BLOCK * 28;
+#else
+using PixAccT = PixAcc;
+constexpr size_t PIX_LDS_BYTES = 0;
+#endif
+
 // Emitter of the GPU trace step: colour -> framebuffer atomics, children -> output queue shard.
 struct GpuEmit {
     const TraceParams& P;
@@ -314,7 +365,7 @@ struct GpuEmit {
     uint32_t shard;
     uint32_t round;
     uint32_t* shadow_acc;
-    PixAcc* acc;  // depth 0: the pixel's sums in the thread (no framebuffer atomics)
+    PixAccT* acc;  // depth 0: the pixel's sums in the thread (no framebuffer atomics)
 
     __device__ void local(d3 c) const {
         if (acc) {
@@ -383,6 +434,28 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
         g.two(j[0], j[1]);
         g.two(j[2], j[3]);
     }
+}
+
+// k_primary's split of primary_uniforms: the pixel-jitter pair (prefetched a sample ahead) and the
+// lens-disk pair (thin-lens cameras only), the same values
+__device__ __forceinline__ void primary_jitter(const TraceParams& P, int s, uint32_t p, uint32_t gpix, double j[2]) {
+    if (P.jitter) {
+        const int64_t plane = P.jit_plane;
+        const double* base = P.jitter + (int64_t)s * 4 * plane + (P.jit_global ? gpix : p);
+        j[0] = base[0];
+        j[1] = base[plane];
+    } else {
+        double j4[4];
+        primary_uniforms(P, s, p, gpix, j4);
+        j[0] = j4[0];
+        j[1] = j4[1];
+    }
+}
+__device__ __forceinline__ void lens_jitter(const TraceParams& P, int s, uint32_t p, uint32_t gpix, double j[4]) {
+    double j4[4] = {0.0, 0.0, 0.0, 0.0};
+    primary_uniforms(P, s, p, gpix, j4);
+    j[2] = j4[2];
+    j[3] = j4[3];
 }
 
 // an emitter whose child replaces the traced ray in place (Em::kInPlace)
@@ -553,7 +626,7 @@ struct FusedEmit {
     const Ray& r;
     uint32_t round;
     uint32_t* shadow_acc;
-    PixAcc* acc;
+    PixAccT* acc;
     Ray* next;
     bool* has;
 
@@ -571,11 +644,9 @@ struct FusedEmit {
 
 // Copy the first `nlut` texture lookup tables into LDS (dynamic shared memory) and point the
 // scene view at them: texel -> value becomes an LDS read instead of a dependent global load.
-__device__ __forceinline__ void stage_luts(TraceParams& P) {
-    extern __shared__ double lds_lut[];
+__device__ __forceinline__ void stage_luts(const TraceParams& P) {
     const int n = P.S.nlut_lds;
-    for (int i = threadIdx.x; i < n * 256; i += BLOCK) lds_lut[i] = P.S.tex[i >> 8].lut[i & 255];
-    P.S.lut_lds = (const RT_LDS double*)lds_lut;
+    for (int i = threadIdx.x; i < n * 256; i += BLOCK) rt_lds_dyn[i] = P.S.tex[i >> 8].lut[i & 255];
     __syncthreads();
 }
 
@@ -608,7 +679,7 @@ __device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3]
 // to the depth-1 queue for k_trace.
 template <uint32_t MATS, int OCC = 2, bool FUSE = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
-    TraceParams P = P0;
+    const TraceParams& P = P0;  // (read in place from the kernel arguments)
     stage_luts(P);
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t err = 0;
@@ -621,6 +692,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     const int s_begin = min(P.spp, grp * spg), s_end = min(P.spp, s_begin + spg);
     const int64_t nwaves = (P.npix + ppw - 1) / ppw;
     const Quot qw((double)P.cam.width), qh((double)P.cam.height);
+#ifdef RT_PIX_LDS
+    RT_LDS unsigned long long* pix_w =
+        (RT_LDS unsigned long long*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256) + threadIdx.x;
+    RT_LDS float* pix_mag = (RT_LDS float*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + 3 * BLOCK) + threadIdx.x;
+#endif
     for (int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); wv < nwaves;
          wv += (int64_t)gridDim.x * (BLOCK / 64)) {
         const int64_t p0 = wv * ppw;
@@ -633,10 +709,17 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
         const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
         const int s_stop = active ? s_end : s_begin;  // (no samples for a lane past the frame's end)
+#ifdef RT_PIX_LDS
+        PixAccT acc{pix_w, pix_mag};
+        acc.zero();
+#else
         PixAcc acc;
-        // software pipeline: the next sample's uniforms are loaded while this sample is traced
-        double jn[4] = {0.0, 0.0, 0.0, 0.0};
-        if (active) primary_uniforms(P, s_begin, p, gpix, jn);
+#endif
+        // software pipeline: the next sample's pixel jitter is loaded while this sample is traced
+        // (the lens-disk pair of a thin-lens camera is loaded when used: two fewer doubles live
+        // across the trace for the pinhole cameras of every example)
+        double jn[2] = {0.0, 0.0};
+        if (active) primary_jitter(P, s_begin, p, gpix, jn);
         for (int s = s_begin; s < s_stop; ++s) {
             Ray r;
             r.o = r.d = d3{0.0, 0.0, 0.0};
@@ -644,9 +727,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             r.meta = pack_meta(0, 0, 0);
             r.pix = p;
             r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
-            const double j[4] = {jn[0], jn[1], jn[2], jn[3]};
+            double j[4] = {jn[0], jn[1], 0.0, 0.0};
             RT_T0(tr0);
-            if (s + 1 < s_stop) primary_uniforms(P, s + 1, p, gpix, jn);
+            if (P.cam.lens_radius != 0.0) lens_jitter(P, s, p, gpix, j);
+            if (s + 1 < s_stop) primary_jitter(P, s + 1, p, gpix, jn);
             primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
             RT_ACC(0, tr0);
             int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
@@ -658,32 +742,36 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
                 // depth's colour into `acc`; the lanes of an iteration share a depth, counted per
                 // wave into the shard's counter of that depth as the queue appends would have been
                 // (the child is written over r: shading reads nothing of the ray after it)
-                bool has = false;
-                trace_one<MATS>(P, r, true, err, hs, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
-                bool live = has;
-                for (int d = 1;; ++d) {
+                // (one loop over the depths, depth 0 included: one inlined copy of the shaders)
+                bool live = true;
+                for (int d = 0;; ++d) {
+                    bool has = false;
+                    trace_one<MATS>(P, r, live, err, d == 0 ? hs : nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
+                    live = live && has;
                     const uint64_t m = __ballot(live);
                     if (m == 0) break;
-                    if (live && lanes_below(m) == 0 && d < SRT_MAX_DEPTHS)  // the lowest live lane
-                        atomicAdd(P.cnt_out + (int64_t)(d - 1) * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
-                    if (d > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
-                    has = false;
-                    trace_one<MATS>(P, r, live, err, nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
-                    live = live && has;
+                    if (live && lanes_below(m) == 0 && d + 1 < SRT_MAX_DEPTHS)  // the lowest live lane
+                        atomicAdd(P.cnt_out + (int64_t)d * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
+                    if (d + 1 > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
                 }
             }
             RT_ACC(3, tt0);
         }
         // the pixel's sample groups (lanes of this wave) summed; lane of group 0 stores the pixel
-        acc.reduce_lanes(fx, ppw);
+#ifdef RT_PIX_LDS
+        PixAcc acc_r = acc.load();
+#else
+        PixAcc& acc_r = acc;
+#endif
+        acc_r.reduce_lanes(fx, ppw);
         const bool owner = pact && grp == 0;
         if (FUSE && P.fuse_resolve) {
             // the frame's only pass: the pixel is complete (scene.py:118-140, k_resolve's rule)
             uint8_t px[3] = {0, 0, 0};
             if (owner) {
-                if (fx && acc.suspect()) atomicOr(&P.flags[1], RETRY_FIXED_RANGE);
+                if (fx && acc_r.suspect()) atomicOr(&P.flags[1], RETRY_FIXED_RANGE);
                 const double spp = (double)P.spp_total;
-                const double rr = acc.value(fx, 0) / spp, gg = acc.value(fx, 1) / spp, bb = acc.value(fx, 2) / spp;
+                const double rr = acc_r.value(fx, 0) / spp, gg = acc_r.value(fx, 1) / spp, bb = acc_r.value(fx, 2) / spp;
                 double a0, a1, a2;
                 resolve_pixel(rr, gg, bb, a0, a1, a2, px);
                 if (P.out_rgb) {
@@ -699,20 +787,20 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             float* mg = fx_mag(P.fbx, P.npix) + p;
             if (P.fb_first) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = acc.w[k];
-                *mg = acc.mag;
+                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = acc_r.w[k];
+                *mg = acc_r.mag;
             } else {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] += acc.w[k];
-                *mg += acc.mag;
+                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] += acc_r.w[k];
+                *mg += acc_r.mag;
             }
         } else if (owner) {
             if (P.fb_first) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] = acc.value(false, k);
+                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] = acc_r.value(false, k);
             } else {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] += acc.value(false, k);
+                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] += acc_r.value(false, k);
             }
         }
     }
@@ -724,7 +812,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
 // b % NSHARD.
 template <uint32_t MATS, int OCC = 2, bool CHAIN = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
-    TraceParams P = P0;
+    const TraceParams& P = P0;
     const uint32_t shard = blockIdx.x % NSHARD;
     const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
     const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
@@ -778,7 +866,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_trace(TraceParams P0) {
 // material.py:42-44), its children appended for the ordinary k_trace depths
 template <uint32_t MATS>
 __global__ __launch_bounds__(BLOCK) void k_shade_forced(TraceParams P0) {
-    TraceParams P = P0;
+    const TraceParams& P = P0;
     const uint32_t shard = blockIdx.x % NSHARD;
     const int64_t n = min((int64_t)P.cnt_in[shard], P.seg);
     const int64_t blk = blockIdx.x / NSHARD, nblk = gridDim.x / NSHARD;
@@ -904,12 +992,10 @@ struct FrameEmit {
 
 template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
-    TraceParams P = P0;
+    const TraceParams& P = P0;
     {
-        extern __shared__ double lds_lut[];
         const int nl = P.S.nlut_lds;
-        for (int i = threadIdx.x; i < nl * 256; i += FRAME_BLOCK) lds_lut[i] = P.S.tex[i >> 8].lut[i & 255];
-        P.S.lut_lds = (const RT_LDS double*)lds_lut;
+        for (int i = threadIdx.x; i < nl * 256; i += FRAME_BLOCK) rt_lds_dyn[i] = P.S.tex[i >> 8].lut[i & 255];
     }
     __shared__ FrameLds L;
     RT_T0(tf0);
@@ -1233,6 +1319,25 @@ __global__ __launch_bounds__(BLOCK) void k_collider_surface(const srt_collider* 
     }
 }
 
+// Material.get_Normal(hit) (material.py:18-36) at points P: the collider's normal, or with a normal
+// map the map's texel (texture 0 of S) through the collider's inverse_basis_matrix, normalised;
+// times the hit orientation
+__global__ __launch_bounds__(BLOCK) void k_material_normal(SceneView S, const srt_collider* c_generic,
+                                                          const srt_material* m_generic, const double* P,
+                                                          const double* orient, int64_t n, double* N,
+                                                          uint32_t* flags) {
+    const RT_RO srt_collider* c = (const RT_RO srt_collider*)c_generic;
+    const RT_RO srt_material* m = (const RT_RO srt_material*)m_generic;
+    uint32_t err = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        const d3 v = shading_normal(S, *c, *m, d3{P[i], P[n + i], P[2 * n + i]}, orient[i], err);
+        N[i] = v.x;
+        N[n + i] = v.y;
+        N[2 * n + i] = v.z;
+    }
+    if (err) atomicOr(flags, err);
+}
+
 // image.get_color(hit): the texel of (u, v) through texture 0 of S (texture.py:27-39)
 __global__ __launch_bounds__(BLOCK) void k_texture_lookup(SceneView S, const double* uv, int64_t n, double* rgb,
                                                          uint32_t* flags) {
@@ -1428,6 +1533,8 @@ struct srt_ctx {
     uint8_t* texels = nullptr;
     uint64_t texel_key = 0;
     int64_t texel_bytes = 0;
+    bool texels_rgbx = false;  // the resident pool holds 3-channel images as RGBX
+    bool texel_rgbx = true;    // option "texel_rgbx": store 3-channel images as RGBX (one dword per texel)
     // camera tables (shared by the slots; uploaded only when they change)
     double* xs = nullptr;
     double* ys = nullptr;
@@ -2250,6 +2357,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "texel_rgbx")) { c->texel_rgbx = value != 0; return SRT_OK; }  // (next srt_upload_scene)
     if (!strcmp(key, "frame_groups")) {
         if (value < 0 || value > 4096) return fail(SRT_ERR_ARG, "frame_groups: 0 (auto) .. 4096");
         c->frame_groups = (int)value;
@@ -2360,9 +2468,43 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     double *media, *f0, *ll, *imp;
     if ((rc = upload(c, d->colliders, d->n_colliders, &col))) return rc;
     if ((rc = upload(c, d->materials, d->n_materials, &mat))) return rc;
-    if ((rc = upload(c, d->textures, d->n_textures, &tex))) return rc;
-    // texel pool: kept in HBM across uploads while the caller's key and size are unchanged
-    if (d->texel_key != 0 && d->texel_key == c->texel_key && d->texel_bytes == c->texel_bytes && c->texels) {
+    // texel pool in HBM: 3-channel images as 4-byte texels (RGBX), so that a texel is one aligned
+    // dword load (texel_rgb) instead of three byte loads; the records point into that layout
+    std::vector<srt_texture> tex_h(d->textures, d->textures + std::max(0, d->n_textures));
+    std::vector<std::array<int64_t, 4>> imgs;  // (offset, bytes, new offset, expand) per image
+    bool rgbx = c->texel_rgbx && d->texel_bytes > 0 && d->texels && !is_device_ptr(d->texels);
+    if (rgbx) {
+        for (const srt_texture& t : tex_h) {
+            const int64_t bytes = (int64_t)t.height * t.width * t.channels;
+            bool seen = false;
+            for (auto& im : imgs)
+                if (im[0] == t.offset) {
+                    seen = true;
+                    rgbx = rgbx && im[1] == bytes;  // (one image per offset, else the pool stays as given)
+                }
+            if (!seen) imgs.push_back({t.offset, bytes, 0, t.channels == 3 ? 1 : 0});
+        }
+        std::sort(imgs.begin(), imgs.end());
+        for (size_t k = 1; k < imgs.size(); ++k) rgbx = rgbx && imgs[k][0] >= imgs[k - 1][0] + imgs[k - 1][1];
+    }
+    int64_t pool_bytes = d->texel_bytes;
+    if (rgbx) {
+        pool_bytes = 0;
+        for (auto& im : imgs) {
+            im[2] = pool_bytes;
+            pool_bytes += ((im[3] ? im[1] / 3 * 4 : im[1]) + 3) / 4 * 4;
+        }
+        for (srt_texture& t : tex_h)
+            for (auto& im : imgs)
+                if (im[0] == t.offset) {
+                    t.offset = im[2];
+                    if (im[3]) t.channels = 4;
+                }
+    }
+    if ((rc = upload(c, tex_h.data(), d->n_textures, &tex))) return rc;
+    // kept in HBM across uploads while the caller's key and size (and the layout) are unchanged
+    if (d->texel_key != 0 && d->texel_key == c->texel_key && d->texel_bytes == c->texel_bytes && c->texels &&
+        rgbx == c->texels_rgbx) {
         texels = c->texels;
     } else {
         if (c->texels) (void)hipFree(c->texels);
@@ -2371,11 +2513,26 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
         c->texel_bytes = 0;
         texels = nullptr;
         if (d->texel_bytes > 0 && d->texels) {
-            HIP_TRY(dalloc(&texels, d->texel_bytes));
-            HIP_TRY(hipMemcpy(texels, d->texels, (size_t)d->texel_bytes, hipMemcpyDefault));
+            HIP_TRY(dalloc(&texels, pool_bytes));
+            if (rgbx) {
+                std::vector<uint8_t> h((size_t)pool_bytes, 0);
+                for (const auto& im : imgs) {
+                    const uint8_t* src = d->texels + im[0];
+                    uint8_t* dst = h.data() + im[2];
+                    if (im[3]) {
+                        for (int64_t i = 0, n = im[1] / 3; i < n; ++i) memcpy(dst + 4 * i, src + 3 * i, 3);
+                    } else {
+                        memcpy(dst, src, (size_t)im[1]);
+                    }
+                }
+                HIP_TRY(hipMemcpy(texels, h.data(), (size_t)pool_bytes, hipMemcpyHostToDevice));
+            } else {
+                HIP_TRY(hipMemcpy(texels, d->texels, (size_t)d->texel_bytes, hipMemcpyDefault));
+            }
             c->texels = texels;
             c->texel_key = d->texel_key;
             c->texel_bytes = d->texel_bytes;
+            c->texels_rgbx = rgbx;
         }
     }
     if ((rc = upload(c, d->lights, d->n_lights, &lights))) return rc;
@@ -2465,6 +2622,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                                  c->shard_snake);
         rows_h = band_rows(cam->height, c->nranks, c->rank, band, c->shard_snake);
         n_rows = (int)rows_h.size();
+        if (n_rows == 0) return fail(SRT_ERR_ARG, "a sharded frame left this rank without rows");
         rows_src = rows_h.data();
     } else if (a->rows) {
         if (is_device_ptr(a->rows)) return fail(SRT_ERR_ARG, "rows must be host memory");
@@ -2853,7 +3011,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
             hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
-                               lut_bytes(c), c->f->stream, P);
+                               lut_bytes(c) + PIX_LDS_BYTES, c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
@@ -3301,6 +3459,64 @@ int srt_texture_lookup(srt_ctx* c, const srt_texture* tex, const uint8_t* texels
     return check_flags(flags);
 }
 
+int srt_material_normal(srt_ctx* c, const srt_collider* col, const srt_texture* normalmap, const uint8_t* texels,
+                        int64_t texel_bytes, const double* P, const double* orient, int64_t n, double* N) {
+    if (!c || !col || !P || !orient || !N) return fail(SRT_ERR_ARG, "null argument");
+    if (col->type < 0 || col->type > 3) return fail(SRT_ERR_ARG, "bad collider type");
+    if (normalmap) {
+        if (!texels || normalmap->offset < 0 || normalmap->channels < 3 || normalmap->channel0 < 0 ||
+            normalmap->channel0 + 3 > normalmap->channels ||
+            normalmap->offset + (int64_t)normalmap->height * normalmap->width * normalmap->channels > texel_bytes)
+            return fail(SRT_ERR_ARG, "normal-map record outside the texel array");
+        if (col->type != SRT_PLANE && col->type != SRT_CUBOID)
+            return fail(SRT_ERR_ARG, "a normal map needs the collider's inverse_basis_matrix (Plane, Cuboid)");
+    }
+    if (n <= 0) return SRT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    srt_material mrec{};
+    mrec.type = SRT_GLOSSY;
+    mrec.tex = mrec.tex_aux0 = mrec.tex_aux1 = -1;
+    mrec.normalmap = normalmap ? 0 : -1;
+    srt_collider* dcol;
+    srt_material* dmat;
+    srt_texture* dtex = nullptr;
+    uint8_t* dtexels = nullptr;
+    double *dP, *dor, *dN;
+    uint32_t* dflags;
+    HIP_TRY(dalloc(&dcol, 1));
+    HIP_TRY(dalloc(&dmat, 1));
+    HIP_TRY(dalloc(&dP, 3 * n));
+    HIP_TRY(dalloc(&dor, n));
+    HIP_TRY(dalloc(&dN, 3 * n));
+    HIP_TRY(dalloc(&dflags, 1));
+    HIP_TRY(hipMemcpy(dcol, col, sizeof(srt_collider), hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dmat, &mrec, sizeof(srt_material), hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dP, P, (size_t)3 * n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(dor, orient, (size_t)n * 8, hipMemcpyDefault));
+    HIP_TRY(hipMemset(dflags, 0, 4));
+    SceneView S{};
+    if (normalmap) {
+        HIP_TRY(dalloc(&dtex, 1));
+        HIP_TRY(dalloc(&dtexels, texel_bytes));
+        HIP_TRY(hipMemcpy(dtex, normalmap, sizeof(srt_texture), hipMemcpyDefault));
+        HIP_TRY(hipMemcpy(dtexels, texels, (size_t)texel_bytes, hipMemcpyDefault));
+        S.tex = (const RT_RO srt_texture*)dtex;
+        S.texels = (const RT_RO uint8_t*)dtexels;
+        S.ntex = 1;
+    }
+    hipLaunchKernelGGL(k_material_normal, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, S, dcol, dmat,
+                       dP, dor, n, dN, dflags);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->f->stream));
+    uint32_t flags = 0;
+    HIP_TRY(hipMemcpy(&flags, dflags, 4, hipMemcpyDefault));
+    HIP_TRY(hipMemcpy(N, dN, (size_t)3 * n * 8, hipMemcpyDefault));
+    void* bufs[] = {dcol, dmat, dP, dor, dN, dflags, dtex, dtexels};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    return check_flags(flags);
+}
+
 int srt_primary_rays(srt_ctx* c, const srt_camera* cam, const double* J, double* O, double* D) {
     if (!c || !cam || !J || !O || !D) return fail(SRT_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
@@ -3436,6 +3652,7 @@ int srt_comm_rank(srt_ctx* c, int* nranks, int* rank) {
 
 }  // extern "C"
 static int render_group_once(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a, srt_stats* st);
+static int render_group_async(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a);
 extern "C" {
 
 int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
@@ -3445,6 +3662,8 @@ int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_ren
             return fail(SRT_ERR_ARG, "contexts must be the ranks 0..n-1 of one srt_comm_init_all group");
     if (a->jitter) return fail(SRT_ERR_ARG, "a group frame draws its jitter on the devices (mt or Philox)");
     if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
+    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_RGB_ROWS)) return fail(SRT_ERR_ARG, "group flags: ASYNC, RGB_ROWS");
+    if (a->flags & SRT_RENDER_ASYNC) return render_group_async(ctxs, n, cam, a);
     // A frame whose passes overflowed a queue/ring, met a chain-mode tie or left the fixed-point range
     // is rendered again on every context (the gather pairs the ranks' tiles), from the same numpy
     // state, as the synchronous single-GPU path does; the contexts already grew their queues or
@@ -3454,9 +3673,12 @@ int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_ren
     int rc = SRT_OK;
     for (int attempt = 0;; ++attempt) {
         if (a->mt) *a->mt = mt0;
+        // (a flag left by an earlier frame must not make a failure of this one look retryable)
+        for (int q = 0; q < n; ++q) ctxs[q]->retry_frame = false;
         rc = render_group_once(ctxs, n, cam, a, st);
         bool again = false;
         for (int q = 0; q < n; ++q) again |= ctxs[q]->retry_frame;
+        if (rc == SRT_OK && st) st->retries += attempt;  // frames rendered again, as srt_render counts them
         if (rc == SRT_OK || !again || attempt >= 8) return rc;
     }
 }
@@ -3513,7 +3735,70 @@ static int render_group_once(srt_ctx** ctxs, int n, const srt_camera* cam, const
     return SRT_OK;
 }
 
+// A pipelined group frame (SRT_RENDER_ASYNC): every context queues its shard (asynchronous
+// srt_render, SRT_RENDER_SHARDED), the uint8 tiles' RCCL gather is posted for all of them in one
+// group, rank 0 assembles the frame and copies it to the caller's out_srgb8 (pinned host memory or
+// device memory of rank 0); the linear RGB goes to out_rgb (pinned host memory visible to every
+// context, srt_host_alloc) either gathered to rank 0 or, with SRT_RENDER_RGB_ROWS, as every rank's
+// rows over its own PCIe link.  Nothing waits: srt_render_group_finish checks every context.
+static int render_group_async(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a) {
+    srt_render_args aq = *a;
+    const bool rows = (a->flags & SRT_RENDER_RGB_ROWS) != 0;
+    aq.flags = SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | (rows ? SRT_RENDER_RGB_ROWS : (a->out_rgb ? SRT_RENDER_GATHER_RGB : 0));
+    int rc = SRT_OK;
+    int queued = 0;
+    for (int q = 0; q < n && !rc; ++q) {
+        aq.out_srgb8 = q == 0 ? a->out_srgb8 : nullptr;
+        aq.out_rgb = (rows || q == 0) ? a->out_rgb : nullptr;
+        ctxs[q]->defer_gather = true;
+        rc = srt_render(ctxs[q], cam, &aq, nullptr);
+        if (!rc) ++queued;
+    }
+    if (!rc && n > 1) {
+        ncclResult_t r = ncclGroupStart();
+        for (int q = 0; q < n && !rc && r == ncclSuccess; ++q) {
+            (void)hipSetDevice(ctxs[q]->device);
+            rc = gather_post(ctxs[q]);
+        }
+        ncclResult_t r2 = ncclGroupEnd();
+        if (!rc && (r != ncclSuccess || r2 != ncclSuccess))
+            rc = fail(SRT_ERR_HIP, std::string("RCCL group gather: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    }
+    if (!rc) {
+        (void)hipSetDevice(ctxs[0]->device);
+        rc = gather_finish(ctxs[0]);
+    }
+    for (int q = 0; q < n; ++q) ctxs[q]->defer_gather = false;
+    if (rc && queued < n) {
+        // a context refused the frame: the others' shards are queued without the gather; wait for them
+        // (their frames are dropped) so that no rank is left a send without its receive
+        for (int q = 0; q < queued; ++q) (void)srt_render_finish(ctxs[q], nullptr);
+    }
+    return rc;
+}
+
 extern "C" {
+
+int srt_render_group_finish(srt_ctx** ctxs, int n, srt_stats* st) {
+    if (!ctxs || n < 1) return fail(SRT_ERR_ARG, "null argument");
+    int rc = SRT_OK;
+    srt_stats sum{};
+    for (int q = 0; q < n; ++q) {
+        srt_stats sq{};
+        const int r = srt_render_finish(ctxs[q], &sq);
+        if (!rc) rc = r;
+        if (q == 0) {
+            sum = sq;
+        } else {
+            for (int d = 0; d < SRT_MAX_DEPTHS; ++d) sum.rays_per_depth[d] += sq.rays_per_depth[d];
+            sum.total_rays += sq.total_rays;
+            sum.shadow_rays += sq.shadow_rays;
+            sum.n_depths = std::max(sum.n_depths, sq.n_depths);
+        }
+    }
+    if (st && !rc) *st = sum;
+    return rc;
+}
 
 int srt_comm_allreduce(srt_ctx* c, double* vals, int n, int op) {
     if (!c || !vals || n < 1 || n > 64 || op < 0 || op > 1) return fail(SRT_ERR_ARG, "bad allreduce arguments");
@@ -3540,7 +3825,7 @@ int srt_comm_barrier(srt_ctx* c) {
 int srt_host_alloc(srt_ctx* c, int64_t bytes, void** out) {
     if (!c || !out || bytes <= 0) return fail(SRT_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocPortable));  // (pinned for every context's device)
     return SRT_OK;
 }
 

@@ -340,6 +340,33 @@ def collider_surface(collider, P, normal=True, uv=True, primitive_uv=False):
     return Nout, uvout
 
 
+def material_normal(material, hit):
+    """Material.get_Normal(hit) on the device (srt_material_normal): the collider normal, or the
+    material's normal map through the collider's inverse_basis_matrix, times hit.orientation (3, n)."""
+    from ._lower import texture_record
+
+    lib, ctx = context()
+    c = hit.collider
+    rec = np.ascontiguousarray(collider_record(c))
+    if getattr(getattr(c, "assigned_primitive", None), "uv_cube_cross", False):
+        rec["flags"] |= N.CF_UV_CROSS  # (the primitive's uv, as hit.get_uv() takes it)
+    Pa = _planar(hit.point)
+    n = Pa.shape[1]
+    orient = np.ascontiguousarray(np.broadcast_to(np.asarray(hit.orientation, dtype=np.float64).reshape(-1)
+                                                  if np.ndim(hit.orientation) else hit.orientation, (n,)))
+    tex, texels = None, None
+    if material.normalmap is not None:
+        if not hasattr(c, "inverse_basis_matrix"):
+            raise AttributeError("'%s' object has no attribute 'inverse_basis_matrix'" % type(c).__name__)
+        tex, texels = texture_record(material.normalmap_u8, material.repeat, linear=False)
+        tex = np.ascontiguousarray(tex).reshape(1)
+    out = np.empty((3, n))
+    N.check(lib, lib.srt_material_normal(ctx, N.ptr(rec.reshape(1)), N.ptr(tex), N.ptr(texels),
+                                         0 if texels is None else texels.size, N.ptr(Pa), N.ptr(orient), n,
+                                         N.ptr(out)))
+    return out
+
+
 def texture_lookup(u8, repeat, u, v, linear=True):
     """image.get_color at (u, v) on the device (srt_texture_lookup): rgb (3, n)."""
     from ._lower import texture_record

@@ -242,6 +242,8 @@ SIGNATURES = {
     "srt_comm_rank": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "srt_render_group": (ctypes.c_int, [_p, ctypes.c_int, ctypes.POINTER(CameraDesc), ctypes.POINTER(RenderArgs),
                                         ctypes.POINTER(Stats)]),
+    "srt_render_group_finish": (ctypes.c_int, [_p, ctypes.c_int, ctypes.POINTER(Stats)]),
+    "srt_material_normal": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int64, _p, _p, ctypes.c_int64, _p]),
     "srt_comm_allreduce": (ctypes.c_int, [_p, _p, ctypes.c_int, ctypes.c_int]),
     "srt_comm_barrier": (ctypes.c_int, [_p]),
     "srt_host_alloc": (ctypes.c_int, [_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]),

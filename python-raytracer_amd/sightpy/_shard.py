@@ -73,6 +73,8 @@ def band_height(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
     best_h, best_rows = 1, None
     for k in range(kmax, max(kmax // 2, 1) - 1, -1):
         h = max(-(-height // (world * k)), 1)
+        if -(-height // h) < world:  # fewer bands than ranks: a rank would get no rows
+            continue
         m = max(rank_rows(height, world, q, h, snake) for q in range(world))
         if best_rows is None or m < best_rows:
             best_h, best_rows = h, m

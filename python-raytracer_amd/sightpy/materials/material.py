@@ -5,7 +5,7 @@ per-batch shading entry point — runs on the device (`srt_shade`): the shading 
 `csrc/rt_device.h` (`rt_shade_*`) implement each subclass, and the reflected / refracted /
 diffuse rays a hit spawns are traced to completion as in get_raycolor.  Normal maps
 (material.py:18-40) are supported for Plane and Cuboid colliders (the only ones with
-`inverse_basis_matrix`).
+`inverse_basis_matrix`), in shading and through get_Normal (srt_material_normal).
 """
 from ..utils.image_functions import load_image_u8
 
@@ -26,10 +26,14 @@ class Material:
         self.repeat = repeat
 
     def get_Normal(self, hit):
-        """Shading normal (material.py:18-36).  Normal-mapped materials shade on the device only."""
-        if self.normalmap is not None:
-            raise NotImplementedError("normal-mapped shading normals are evaluated inside srt_shade / srt_render")
-        return hit.collider.get_Normal(hit) * hit.orientation
+        """Shading normal (material.py:18-36) at hit.point on the device (srt_material_normal): the
+        collider's normal, or the normal map's texel at the primitive's uv through the collider's
+        inverse_basis_matrix, normalised; times the hit orientation."""
+        from .._backend import material_normal
+        from ..utils.vector3 import vec3
+
+        N = material_normal(self, hit)
+        return vec3(N[0], N[1], N[2])
 
     def get_color(self, scene, ray, hit):
         """Colour of the batch `ray` at `hit` (all rays hit `hit.collider` at `hit.distance` with

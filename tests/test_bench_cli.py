@@ -1,9 +1,9 @@
 """bench.py --gpus N on the CPU: N means N GPUs or an error, never a silent 1-GPU line.
 
-  * WORLD_SIZE unset, N > 1: bench.py starts N ranks through torch.distributed.run as a child
-    process (one process per GPU, nothing in the parent touches the GPU), after checking that N GPUs
-    are visible (counted from the KFD topology, without initialising HIP);
-  * under a launcher: WORLD_SIZE must equal N;
+  * WORLD_SIZE unset, N > 1: bench.py drives the N GPUs from this one process through the library's
+    own multi-GPU group (srt_comm_init_all + pipelined srt_render_group; no torch, no launcher), after
+    checking that N GPUs are visible (counted from the KFD topology, without initialising HIP);
+  * under a launcher (one process per GPU): WORLD_SIZE must equal N;
   * fewer GPUs than N, or a mismatch: rc != 0 and no JSON line.
 """
 import json
@@ -49,11 +49,7 @@ def test_launch_plan(bench):
         bench.launch_plan(4, {"WORLD_SIZE": "2"}, 8, [])
     with pytest.raises(SystemExit, match="only 3 GPU"):
         bench.launch_plan(4, {}, 3, [])
-    cmd = bench.launch_plan(8, {}, 8, ["--gpus", "8", "--steps", "5"])
-    i = cmd.index("torch.distributed.run")
-    assert cmd[i - 1] == "-m" and cmd[i + 1:i + 4] == ["--nnodes=1", "--nproc-per-node", "8"]
-    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
-    assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")
+    assert bench.launch_plan(8, {}, 8, ["--gpus", "8", "--steps", "5"]) == bench.GROUP
 
 
 def test_visible_gpus_honours_visibility_lists(bench, monkeypatch):
@@ -65,28 +61,37 @@ def test_visible_gpus_honours_visibility_lists(bench, monkeypatch):
     assert bench.visible_gpus() == min(n, 2)
 
 
-def test_gpus_2_with_mocked_count_launches_two_ranks(bench, monkeypatch, capsys):
-    """With 2 GPUs 'visible' (mocked) the bench starts 2 ranks through torch.distributed.run; here the
-    ranks find no GPU and fail, so the job fails -- it does not fall back to a 1-GPU line."""
+def test_gpus_2_with_mocked_count_runs_the_group_in_process(bench, monkeypatch, capsys):
+    """With 2 GPUs 'visible' (mocked) and no launcher, main() runs the in-process group plan with N = 2
+    and prints its line; nothing goes through torch.distributed.run or a second process."""
     monkeypatch.setattr(bench, "visible_gpus", lambda: 2)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
     seen = {}
-    real_run = subprocess.run
 
-    def spy(cmd, *a, **kw):
-        seen["cmd"] = cmd
-        kw.setdefault("capture_output", True)
-        kw.setdefault("timeout", 240)
-        r = real_run(cmd, *a, text=True, **kw)
-        seen["out"] = r.stdout
-        return r
+    def fake_group(args, gpus):
+        seen["gpus"] = gpus
+        seen["steps"] = args.steps
+        return {"metric": "m", "n_gpus": gpus, "nranks": gpus}
 
-    monkeypatch.setattr(bench.subprocess, "run", spy)
-    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"])
-    with pytest.raises(SystemExit) as e:
-        bench.main()
-    assert e.value.code != 0
-    assert "--nproc-per-node" in seen["cmd"] and seen["cmd"][seen["cmd"].index("--nproc-per-node") + 1] == "2"
-    lines = [json.loads(ln) for ln in seen["out"].splitlines() if ln.startswith("{")]
-    assert not any(d.get("n_gpus") == 1 for d in lines)
+    def no_subprocess(*a, **kw):
+        raise AssertionError("no child process expected: %r" % (a,))
+
+    monkeypatch.setattr(bench, "run_group", fake_group)
+    monkeypatch.setattr(bench.subprocess, "run", no_subprocess)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "0", "--no-cpu-baseline"])
+    bench.main()
+    assert seen == {"gpus": 2, "steps": 3}
+    lines = [json.loads(ln) for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
+    assert lines == [{"metric": "m", "n_gpus": 2, "nranks": 2}]
+
+
+def test_gpus_2_group_without_gpus_fails_without_a_line(tmp_path):
+    """The in-process group plan with 2 GPUs 'visible' (HIP sees none here): srt_comm_init_all fails,
+    the run fails, and no JSON line (in particular no 1-GPU line) is printed."""
+    code = ("import sys; sys.argv = ['bench.py', '--gpus', '2', '--steps', '1', '--warmup', '0', '--no-cpu-baseline'];"
+            "sys.path.insert(0, %r); import bench; bench.visible_gpus = lambda: 2; bench.main()" % str(ROOT))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=_env(), cwd=str(tmp_path),
+                       timeout=120)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -232,3 +232,70 @@ def test_gpu_shade_rejects_foreign_collider_index():
     ray = Ray(vec3(*Ob), vec3(*Do), 0, sc.n, 0, 0, 0)
     with pytest.raises(IndexError):
         _backend().trace_rays(ray, sc, hits=(len(sc.collider_list), np.ones(48), np.ones(48)))
+
+
+def _primary_hits(sc, ci, seed=5):
+    """Points where one sample of primary rays of `sc` hits collider index `ci` nearest, with the
+    orientations there (oracle nearest hit)."""
+    np.random.seed(seed)
+    jit = sc.camera.draw_jitter(1)[0]
+    Oo, Do = O.primary_rays(sc.camera, jit)
+    Ob = np.ascontiguousarray(np.broadcast_to(Oo, Do.shape))
+    near, ids = O.hit_ids(sc, Ob, Do)
+    sel = ids == ci
+    t, orient = O.intersect(sc.collider_list[ci], Ob[:, sel], Do[:, sel])
+    return Ob[:, sel] + Do[:, sel] * t, orient
+
+
+@pytest.mark.parametrize("which", ["floor_plane", "rotated_cuboid", "plain_sphere"])
+def test_gpu_material_get_normal_matches_oracle(which):
+    """Material.get_Normal(hit) (material.py:18-36) through srt_material_normal: the normal-mapped
+    floor of the features scene (the map's texel at the primitive's uv, through the Plane's
+    inverse_basis_matrix), a normal-mapped rotated Cuboid (its 4x3 cross uv and basis), and a plain
+    material (collider normal x orientation) -- against the oracle's shading_normal."""
+    from sightpy import Cuboid, Glossy, rgb, vec3
+
+    sc = scenes.features(96, 72, 3)
+    if which == "floor_plane":
+        ci = 0
+    elif which == "plain_sphere":
+        ci = 3
+    else:
+        m = Glossy(diff_color=rgb(0.5, 0.4, 0.3), n=vec3(1.5 + 0j, 1.5 + 0j, 1.5 + 0j), roughness=0.3)
+        m.set_normalmap("floor.jpg", repeat=2.0)
+        cb = Cuboid(material=m, center=vec3(0.2, 0.2, 0.5), width=0.9, height=0.7, length=0.8, max_ray_depth=3)
+        cb.rotate(θ=35, u=vec3(0.3, 1, 0.2))
+        sc.add(cb)
+        ci = len(sc.collider_list) - 1
+    c = sc.collider_list[ci]
+    mat = c.assigned_primitive.material
+    P, orient = _primary_hits(sc, ci)
+    assert P.shape[1] > 64
+    from sightpy import Hit
+
+    h = Hit(None, orient, mat, c, c.assigned_primitive)
+    h.point = vec3(P[0], P[1], P[2])
+    got = mat.get_Normal(h)
+    got = np.stack([got.x, got.y, got.z])
+    ref = O.shading_normal(mat, c, P, orient)
+    np.testing.assert_allclose(got, ref, rtol=FTOL, atol=1e-15)
+    if which != "plain_sphere":
+        # the map moved the normals off the collider's (so the texel path was exercised)
+        plain = np.broadcast_to(O.collider_normal(c, P), P.shape) * orient
+        assert np.abs(got - plain).max() > 1e-3
+
+
+def test_gpu_material_get_normal_needs_inverse_basis_like_reference():
+    """A normal-mapped material on a Sphere: the reference reads hit.collider.inverse_basis_matrix,
+    which a Sphere_Collider lacks (AttributeError); so does this."""
+    from sightpy import Glossy, Hit, rgb, vec3
+
+    sc = scenes.features(64, 48, 3)
+    c = sc.collider_list[3]
+    m = Glossy(diff_color=rgb(0.5, 0.4, 0.3), n=vec3(1.5 + 0j, 1.5 + 0j, 1.5 + 0j))
+    m.set_normalmap("floor.jpg")
+    P, orient = _primary_hits(sc, 3)
+    h = Hit(None, orient, m, c, c.assigned_primitive)
+    h.point = vec3(P[0], P[1], P[2])
+    with pytest.raises(AttributeError):
+        m.get_Normal(h)

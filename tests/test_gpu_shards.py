@@ -68,10 +68,10 @@ def test_example4_4k_d6_rank_of_8_full_width_matches_oracle(rank):
 
 @pytest.mark.parametrize("rank", [3])
 def test_cornell_800_rank_of_8_full_width_matches_oracle_device_stream(rank):
-    from sightpy._shard import shard_rows
+    from sightpy._shard import scene_fanout, shard_rows
 
     sc = scenes.cornell(800, 800)
-    rows = shard_rows(800, 8, rank)
+    rows = shard_rows(800, 8, rank, fanout=scene_fanout(sc))  # (the library's 2-row bands of a fan-out scene)
     np.random.seed(8)
     jit = sc.camera.draw_jitter(1)
     out, rgb, ids, counts = _render_shard(sc, jit, rows, seed=2025, stream=O.DeviceStream(2025))
@@ -81,3 +81,53 @@ def test_cornell_800_rank_of_8_full_width_matches_oracle_device_stream(rank):
     worst = assert_rel_no_floor(out.rgb, rgb)
     print("cornell 800x800 rank %d of 8: %d rays, worst relative RGB error %.3e" % (rank, out.stats["total_rays"],
                                                                                       worst))
+
+
+# ---- multi-pass accumulation at the 8-GPU configurations ------------------------------------------
+# The multi-GPU frames run several passes per frame (cornell 512 spp: 11 passes; ex4 10 spp): the
+# first pass stores the pixels' fixed-point sums, later passes add to them.  batch_size=1 forces one
+# pass per sample on a few full-width rows of a rank's shard, compared with the oracle.
+
+
+def test_cornell_800_multipass_band_of_rank_3_matches_oracle_device_stream():
+    """One 2-row band of rank 3's shard of the 8-rank cornell frame (800 wide), 4 spp in 4 passes
+    (batch_size 1), Monte-Carlo draws from the device stream the oracle restates
+    (reference example_cornellbox.py:126 renders 100 spp; the BASELINE config 512)."""
+    from sightpy._shard import scene_fanout, shard_rows
+
+    sc = scenes.cornell(800, 800)
+    rows = shard_rows(800, 8, 3, fanout=scene_fanout(sc))[:2]
+    assert rows[1] == rows[0] + 1  # one band
+    np.random.seed(13)
+    jit = sc.camera.draw_jitter(4)
+    from sightpy import _backend as B
+
+    part = np.ascontiguousarray(jit.reshape(4, 4, 800, 800)[:, :, rows].reshape(4, 4, -1))
+    out = B.render_scene(sc, 4, jitter=part, seed=77, rows=rows, batch_size=1, want_hits=True)
+    assert out.stats["passes"] == 4
+    rgb, ids, counts = O.render_linear(sc, part, stream=O.DeviceStream(77), rows=rows)
+    assert np.array_equal(out.hit_ids, ids)
+    assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+    worst = assert_rel_no_floor(out.rgb, rgb)
+    print("cornell 800 rank 3 band, 4 spp in 4 passes: worst relative RGB error %.3e" % worst)
+
+
+def test_example4_4k_multipass_rows_of_rank_5_match_oracle():
+    """Four 3840-wide rows of rank 5's shard of the 8-rank ex4 frame, 3 spp in 3 passes (batch_size 1)
+    on the reference's numpy stream (example4.py:34 renders 10 spp)."""
+    from sightpy._shard import shard_rows
+
+    sc = scenes.example4(3840, 2160, 6)
+    rows = shard_rows(2160, 8, 5)[:4]
+    np.random.seed(14)
+    jit = sc.camera.draw_jitter(3)
+    from sightpy import _backend as B
+
+    part = np.ascontiguousarray(jit.reshape(3, 4, 2160, 3840)[:, :, rows].reshape(3, 4, -1))
+    out = B.render_scene(sc, 3, jitter=part, seed=1, rows=rows, batch_size=1, want_hits=True)
+    assert out.stats["passes"] == 3
+    rgb, ids, counts = O.render_linear(sc, part, rows=rows)
+    assert np.array_equal(out.hit_ids, ids)
+    assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+    worst = assert_rel_no_floor(out.rgb, rgb)
+    print("example4 4K rank 5 rows, 3 spp in 3 passes: worst relative RGB error %.3e" % worst)

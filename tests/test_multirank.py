@@ -78,7 +78,7 @@ def _kernel_shard_map(H, n, kmax=8, snake=None):
     return owner, local, h
 
 
-@pytest.mark.parametrize("H", [8, 37, 300, 800, 1080, 2160])
+@pytest.mark.parametrize("H", [8, 9, 13, 37, 300, 800, 1080, 2160])
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("kmax", [1, 4, 8, 17])
 @pytest.mark.parametrize("snake", [0, 1])
@@ -89,6 +89,7 @@ def test_kernel_shard_map_matches_partition(H, n, kmax, snake):
     assert h == band_height(H, n, kmax, snake)
     for q in range(n):
         rows = shard_rows(H, n, q, kmax, snake)
+        assert len(rows) > 0  # (H >= n) every rank gets rows, e.g. H = 9 over 8 ranks with one band each
         assert len(rows) == rank_rows(H, n, q, h, snake)
         assert np.array_equal(np.where(owner == q)[0], rows)
         assert np.array_equal(local[rows], np.arange(len(rows)))
@@ -268,6 +269,63 @@ def test_gpu_group_render_one_device_equals_plain_render(monkeypatch):
     np.testing.assert_allclose(got.rgb, ref.rgb, rtol=1e-12, atol=1e-15)
     assert np.array_equal(got.srgb8, ref.srgb8)
     assert got.stats["total_rays"] == ref.stats["total_rays"]
+
+
+@pytest.mark.gpu
+def test_gpu_async_group_frames_equal_plain_render(monkeypatch):
+    """Pipelined group frames (srt_render_group with SRT_RENDER_ASYNC | SRT_RENDER_RGB_ROWS, then
+    srt_render_group_finish: the in-process multi-GPU bench's frame loop, bench.py --gpus N) on a group
+    of one device: every frame's uint8 image and linear RGB in pinned host memory equal the synchronous
+    render from the same numpy state, and the numpy stream continues frame to frame as Scene.render's."""
+    import ctypes
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    monkeypatch.setenv("SIGHTPY_DEVICES", str(B.devices()[0]))
+    sc = scenes.example1(96, 64, 4)
+    W, H = 96, 64
+    np.random.seed(8)
+    refs = [B.render_scene(sc, 2, seed=5, mt=True) for _ in range(3)]
+    lib, ctxs = B.group()
+    c0 = ctypes.c_void_p(ctxs[0])
+    B.upload(sc, ctx=c0)
+    cd = B.camera_desc(sc.camera)
+    bufs = []
+    for _ in range(3):
+        pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(lib, lib.srt_host_alloc(c0, 3 * W * H, ctypes.byref(pu)))
+        N.check(lib, lib.srt_host_alloc(c0, 3 * W * H * 8, ctypes.byref(pr)))
+        bufs.append((pu, pr))
+    try:
+        np.random.seed(8)
+        mt = N.MtState.from_numpy()
+        a = N.RenderArgs()
+        a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, H, 0
+        a.rows, a.jitter, a.out_hit_id = None, None, None
+        a.mt = ctypes.pointer(mt)
+        a.seed = 5
+        a.flags = N.RENDER_ASYNC | N.RENDER_RGB_ROWS
+        for pu, pr in bufs:
+            a.out_srgb8, a.out_rgb = pu, pr
+            N.check(lib, lib.srt_render_group(ctxs, 1, ctypes.byref(cd), ctypes.byref(a), None))
+        st = N.Stats()
+        N.check(lib, lib.srt_render_group_finish(ctxs, 1, ctypes.byref(st)))
+        assert st.as_dict()["total_rays"] == refs[-1].stats["total_rays"]
+        for (pu, pr), ref in zip(bufs, refs):
+            u8 = np.ctypeslib.as_array(ctypes.cast(pu, ctypes.POINTER(ctypes.c_uint8)), (H, W, 3)).copy()
+            rgb = np.ctypeslib.as_array(ctypes.cast(pr, ctypes.POINTER(ctypes.c_double)), (3, W * H)).copy()
+            assert np.array_equal(u8, ref.srgb8)
+            assert np.array_equal(rgb, ref.rgb)
+        np.random.seed(8)
+        for _ in range(3):
+            np.random.rand(3 * 4 * W * H)  # each frame: 2 samples + the sizing draw (scene.py:78-81)
+        assert np.array_equal(np.random.get_state()[1], np.ctypeslib.as_array(mt.key))
+        assert np.random.get_state()[2] == mt.pos
+    finally:
+        for pu, pr in bufs:
+            lib.srt_host_free(c0, pu)
+            lib.srt_host_free(c0, pr)
 
 
 @pytest.mark.gpu
