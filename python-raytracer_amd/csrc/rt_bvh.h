@@ -26,7 +26,7 @@ namespace rt {
 
 constexpr int BVH_MIN_TRIANGLES = 8;  // fewer triangles stay in the linear collider loop
 constexpr int BVH_LEAF = 4;
-constexpr int BVH_MAX_DEPTH = 30;  // binary levels (so at most 30 4-wide levels: 91 stack entries < BVH_STACK)
+constexpr int BVH_MAX_DEPTH = 20;  // binary levels (so at most 20 4-wide levels: 61 stack entries <= BVH_STACK)
 static_assert(3 * BVH_MAX_DEPTH + 1 <= BVH_STACK, "traversal stack holds the deepest path");
 
 struct BvhBuild {

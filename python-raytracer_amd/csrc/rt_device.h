@@ -236,7 +236,7 @@ struct SceneView {
     const RT_RO struct BvhNode* bvh;
     const RT_RO int32_t* bvh_tri;  // collider index of each BVH leaf slot
     int bvh_nodes;                 // 0: no BVH
-    int pad_;
+    int sky_col;                   // the one collider shaded by a SkyBox / Panorama material, else -1
 };
 // the host builds SceneView/TraceParams and the device reads them: the layout must agree
 static_assert(sizeof(SceneView) == 176 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
@@ -253,7 +253,7 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 128, "one 128-byte line per BVH node");
 constexpr int32_t BVH_EMPTY = (int32_t)0x80000000;
-constexpr int BVH_STACK = 96;  // (3 entries per 4-wide level at most: depth <= 30 levels)
+constexpr int BVH_STACK = 64;  // (3 entries per 4-wide level at most: depth <= 20 levels)
 
 // The kernel's dynamic LDS: the texture tables [0, nlut_lds) staged by the trace kernels first
 // (rt_kernels.hip stage_luts), read directly (no pointer in the scene view, so the kernels' scene view
@@ -621,13 +621,13 @@ RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear)
 RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
     const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
     int stack[BVH_STACK];
-    double stn[BVH_STACK];
+    float stn[BVH_STACK];  // entry distances rounded down (a lower bound: prunes no box that holds a hit)
     int sp = 0;
     stack[sp] = 0;
     stn[sp++] = -INFINITY;
     while (sp > 0) {
         --sp;
-        if (stn[sp] > best) continue;
+        if ((double)stn[sp] > best) continue;
         const RT_RO BvhNode& nd = S.bvh[stack[sp]];
         int in[4];
         double it[4];
@@ -660,8 +660,10 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
             }
         }
         for (int j = 0; j < ni && sp < BVH_STACK; ++j) {
+            float f = (float)it[j];
+            if ((double)f > it[j]) f = nextafterf(f, -INFINITY);
             stack[sp] = in[j];
-            stn[sp++] = it[j];
+            stn[sp++] = f;
         }
     }
 }
@@ -1016,6 +1018,53 @@ RT_HD void shade_sky(const SceneView& S, const RT_RO srt_collider& c, int mi, co
         col = d3{col.x + m.p[0] * lt.x, col.y + m.p[0] * lt.y, col.z + m.p[0] * lt.z};
     }
     em.local(col);
+}
+
+// The collider whose material is the scene's SkyBox / Panorama (SceneView::sky_col), when exactly one
+// collider has a sky material; else -1
+RT_HD int sky_collider(const srt_collider* col, int n, const srt_material* mat) {
+    int k = -1;
+    for (int i = 0; i < n; ++i)
+        if (mat[col[i].material].type == SRT_SKY) {
+            if (k >= 0) return -1;
+            k = i;
+        }
+    return k;
+}
+
+// A texel's 4 bytes as one word (texel_rgb's layouts): one dword load for RGBX / RGBA texels
+RT_HD uint32_t texel_word(const RT_RO srt_texture& T, const RT_RO uint8_t* px) {
+    if (T.channels == 4 && T.channel0 == 0) return *reinterpret_cast<const RT_RO uint32_t*>(px);
+    return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+}
+RT_HD d3 word_rgb(const SceneView& S, int tid, uint32_t w) {
+    return d3{tex_lut(S, tid, (uint8_t)(w & 0xFFu)), tex_lut(S, tid, (uint8_t)((w >> 8) & 0xFFu)),
+              tex_lut(S, tid, (uint8_t)((w >> 16) & 0xFFu))};
+}
+
+// shade_sky in two halves around the waterfall of the other colliders (trace_one): the texel words
+// of a sky hit (colour, and the lightmap's on a non-primary ray) fetched first, so their load latency
+// overlaps the other colliders' shading; the colour made from them afterwards -- the same values
+// shade_sky computes (skybox.py:51-94)
+RT_HD void sky_fetch(const SceneView& S, const Ray& r, double t, uint32_t& w0, uint32_t& w1, uint32_t& err) {
+    const RT_RO srt_collider& c = S.col[S.sky_col];
+    const RT_RO srt_material& m = S.mat[c.material];
+    const d3 P = add(r.o, mul(r.d, t));
+    double u, v;
+    if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
+    w0 = texel_word(S.tex[m.tex], tex_uv(S, S.tex[m.tex], u, v, err));
+    w1 = 0u;
+    if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP))
+        w1 = texel_word(S.tex[m.tex_aux0], tex_uv(S, S.tex[m.tex_aux0], u, v, err));
+}
+RT_HD d3 sky_color(const SceneView& S, const Ray& r, uint32_t w0, uint32_t w1) {
+    const RT_RO srt_material& m = S.mat[S.col[S.sky_col].material];
+    d3 col = word_rgb(S, m.tex, w0);
+    if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP)) {
+        const d3 lt = word_rgb(S, m.tex_aux0, w1);
+        col = d3{col.x + m.p[0] * lt.x, col.y + m.p[0] * lt.y, col.z + m.p[0] * lt.z};
+    }
+    return col;
 }
 
 // Emissive.get_color (emissive.py:21-23)

@@ -57,6 +57,7 @@ SceneView view_of(const srt_scene_desc* d) {
     S.importance = d->importance;
     S.ncol = d->n_colliders; S.nmat = d->n_materials; S.ntex = d->n_textures; S.nlights = d->n_lights;
     S.nmedia = d->n_media; S.nimp = d->n_importance;
+    S.sky_col = sky_collider(d->colliders, d->n_colliders, d->materials);
     S.nshadow = 0;
     for (int i = 0; i < d->n_colliders; ++i)
         if (d->colliders[i].flags & SRT_CF_SHADOW) S.nshadow++;

@@ -357,6 +357,11 @@ constexpr size_t PIX_LDS_BYTES = (size_t)BLOCK * 28;
 using PixAccT = PixAcc;
 constexpr size_t PIX_LDS_BYTES = 0;
 #endif
+#ifdef RT_COLD_LDS
+constexpr size_t COLD_LDS_BYTES = (size_t)BLOCK * 24;  // k_primary: xc, yr (f64), global pixel (u32) per thread
+#else
+constexpr size_t COLD_LDS_BYTES = 0;
+#endif
 
 // Emitter of the GPU trace step: colour -> framebuffer atomics, children -> output queue shard.
 struct GpuEmit {
@@ -510,7 +515,16 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     // copy of the shaders per kernel (a separate tie loop held a second one: the kernels waited on
     // instruction fetch ~10 % of their wave cycles, SQ_WAIT_INST_ANY).
     RT_T0(tw0);
-    int cur = id;     // collider this lane shades next (-1: done)
+    // a SkyBox / Panorama hit without a tie: its texel words fetched now, its colour added after the
+    // waterfall of the other colliders (the load latency overlaps their shading; fixed-point sums do
+    // not depend on the order of the terms)
+    bool sky_pre = false;
+    uint32_t sky_w0 = 0u, sky_w1 = 0u;
+    if constexpr (!FORCED && (MATS & mat_bit(SRT_SKY)) != 0) {
+        sky_pre = S.sky_col >= 0 && id == S.sky_col && !ties;
+        if (sky_pre) sky_fetch(S, r, t, sky_w0, sky_w1, err);
+    }
+    int cur = sky_pre ? -1 : id;  // collider this lane shades next (-1: done)
     double co = o;    // its orientation
     uint32_t rnd = 0;  // emission round: 0 the nearest collider, k the k-th tied one
     uint64_t pending = __ballot(cur >= 0);
@@ -572,6 +586,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
         }
         pending = __ballot(cur >= 0);
     }
+    if (sky_pre) em0.local(sky_color(S, r, sky_w0, sky_w1));
     RT_ACC(2, tw0);
 }
 
@@ -697,6 +712,16 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         (RT_LDS unsigned long long*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256) + threadIdx.x;
     RT_LDS float* pix_mag = (RT_LDS float*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + 3 * BLOCK) + threadIdx.x;
 #endif
+#ifdef RT_COLD_LDS
+    // the item's per-pixel values read once per sample (camera grid coordinates, global pixel) kept in
+    // LDS instead of registers live across the trace: read back with relaxed atomic loads, which the
+    // compiler neither hoists nor keeps
+    RT_LDS double* cold_d = (RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + PIX_LDS_BYTES / 8 + threadIdx.x;
+    RT_LDS uint32_t* cold_u = (RT_LDS uint32_t*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + PIX_LDS_BYTES / 8 +
+                                                 2 * BLOCK) + threadIdx.x;
+#define COLD_D(k) __hip_atomic_load(cold_d + (k) * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define COLD_U(k) __hip_atomic_load(cold_u + (k) * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#endif
     for (int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); wv < nwaves;
          wv += (int64_t)gridDim.x * (BLOCK / 64)) {
         const int64_t p0 = wv * ppw;
@@ -706,8 +731,17 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         const uint32_t lr = pact ? p / (uint32_t)P.cam.width : 0u;
         const uint32_t col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
         const int grow = pact ? P.rows[lr] : 0;
+#ifdef RT_COLD_LDS
+        cold_d[0] = pact ? P.cam.xs[col] : 0.0;
+        cold_d[BLOCK] = pact ? P.cam.ys[grow] : 0.0;
+        cold_u[0] = (uint32_t)grow * (uint32_t)P.cam.width + col;
+#define xc COLD_D(0)
+#define yr COLD_D(1)
+#define gpix COLD_U(0)
+#else
         const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
         const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
+#endif
         const int s_stop = active ? s_end : s_begin;  // (no samples for a lane past the frame's end)
 #ifdef RT_PIX_LDS
         PixAccT acc{pix_w, pix_mag};
@@ -757,6 +791,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             }
             RT_ACC(3, tt0);
         }
+#ifdef RT_COLD_LDS
+#undef xc
+#undef yr
+#undef gpix
+#endif
         // the pixel's sample groups (lanes of this wave) summed; lane of group 0 stores the pixel
 #ifdef RT_PIX_LDS
         PixAcc acc_r = acc.load();
@@ -1535,6 +1574,7 @@ struct srt_ctx {
     int64_t texel_bytes = 0;
     bool texels_rgbx = false;  // the resident pool holds 3-channel images as RGBX
     bool texel_rgbx = true;    // option "texel_rgbx": store 3-channel images as RGBX (one dword per texel)
+    bool sky_prefetch = true;  // option "sky_prefetch" (next srt_upload_scene): trace_one's early sky texel fetch
     // camera tables (shared by the slots; uploaded only when they change)
     double* xs = nullptr;
     double* ys = nullptr;
@@ -2358,6 +2398,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
     if (!strcmp(key, "texel_rgbx")) { c->texel_rgbx = value != 0; return SRT_OK; }  // (next srt_upload_scene)
+    if (!strcmp(key, "sky_prefetch")) { c->sky_prefetch = value != 0; return SRT_OK; }  // (next srt_upload_scene)
     if (!strcmp(key, "frame_groups")) {
         if (value < 0 || value > 4096) return fail(SRT_ERR_ARG, "frame_groups: 0 (auto) .. 4096");
         c->frame_groups = (int)value;
@@ -2547,6 +2588,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     S.light_local = (decltype(S.light_local))ll; S.importance = (decltype(S.importance))imp;
     S.ncol = d->n_colliders; S.nmat = d->n_materials; S.ntex = d->n_textures; S.nlights = d->n_lights;
     S.nmedia = d->n_media; S.nimp = d->n_importance;
+    S.sky_col = c->sky_prefetch ? sky_collider(d->colliders, d->n_colliders, d->materials) : -1;
     S.nshadow = 0;
     {
         // triangle meshes: BVH over the Triangle colliders, the rest intersected one by one
@@ -3011,7 +3053,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
             hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
-                               lut_bytes(c) + PIX_LDS_BYTES, c->f->stream, P);
+                               lut_bytes(c) + PIX_LDS_BYTES + COLD_LDS_BYTES, c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
