@@ -496,6 +496,16 @@ RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err)
     return texel_rgb(S, T, tid, tex_uv(S, T, u, v, err));
 }
 
+// A texel's 4 bytes as one word (texel_rgb's layouts): one dword load for RGBX / RGBA texels
+RT_HD uint32_t texel_word(const RT_RO srt_texture& T, const RT_RO uint8_t* px) {
+    if (T.channels == 4 && T.channel0 == 0) return *reinterpret_cast<const RT_RO uint32_t*>(px);
+    return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+}
+RT_HD d3 word_rgb(const SceneView& S, int tid, uint32_t w) {
+    return d3{tex_lut(S, tid, (uint8_t)(w & 0xFFu)), tex_lut(S, tid, (uint8_t)((w >> 8) & 0xFFu)),
+              tex_lut(S, tid, (uint8_t)((w >> 16) & 0xFFu))};
+}
+
 // Material.get_Normal (material.py:18-36): collider normal (or normal map) times orientation
 RT_HD d3 shading_normal(const SceneView& S, const RT_RO srt_collider& c, const RT_RO srt_material& m, d3 P,
                         double orient, uint32_t& err) {
@@ -828,20 +838,40 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
     RT_T0(tg0);
     d3 P = add(r.o, mul(r.d, t));
     d3 N = shading_normal(S, c, m, P, orient, err);
-    d3 diff;
+    // the texel word of a textured material is loaded first and read after the shadow tests of the
+    // lights (which do not depend on it), so its latency overlaps them; the colour is then composed
+    // in the reference's order (glossy.py:30-84)
+    uint32_t tw = 0u;
     if (m.tex >= 0) {
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
-        diff = mul(tex_rgb(S, m.tex, u, v, err), m.p[3]);
-    } else {
-        diff = ld3(m.p);
+        tw = texel_word(S.tex[m.tex], tex_uv(S, S.tex[m.tex], u, v, err));
     }
     RT_ACC(4, tg0);
     RT_T0(tg1);
-    d3 color = mul(ld3(S.ambient), diff);
     d3 V = mul(r.d, -1.0);
     d3 nudged = add(P, mul(N, NUDGE));
     uint32_t med = meta_medium(r.meta);
+    // seelight of the first 32 lights (glossy.py:53-59), tested before the texel is read
+    uint32_t see = 0u;
+    for (int l = 0; l < S.nlights && l < 32; ++l) {
+        const RT_RO srt_light& Lt = S.lights[l];
+        if (Lt.type != SRT_LIGHT_DIRECTIONAL) continue;
+#ifndef RT_ABL_SHADOW  // (diagnostic build only: time without the shadow test)
+        if (S.nshadow > 0) {
+            RT_T0(ts0);
+            const double ln = shadow_nearest<BVH>(S, l, nudged, ld3(Lt.dir), SKYBOX_DISTANCE);
+            RT_ACC(5, ts0);
+            if (ln >= SKYBOX_DISTANCE) see |= 1u << l;
+            em.shadow(1);
+        } else
+#endif
+        {
+            see |= 1u << l;
+        }
+    }
+    const d3 diff = m.tex >= 0 ? mul(word_rgb(S, m.tex, tw), m.p[3]) : ld3(m.p);
+    d3 color = mul(ld3(S.ambient), diff);
     for (int l = 0; l < S.nlights; ++l) {
         const RT_RO srt_light& Lt = S.lights[l];
         if (Lt.type != SRT_LIGHT_DIRECTIONAL) {
@@ -856,16 +886,14 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
         const d3 lv = mul(ld3(Lt.color), NdotL);
         d3 H = normalize(add(L, V));
         double seelight = 1.0;
-#ifdef RT_ABL_SHADOW  // diagnostic build only: time without the shadow test
-        if (false) {
-#else
-        if (S.nshadow > 0) {
-#endif
-            RT_T0(ts0);
+        if (l < 32) {
+            seelight = ((see >> l) & 1u) ? 1.0 : 0.0;
+#ifndef RT_ABL_SHADOW
+        } else if (S.nshadow > 0) {
             double ln = shadow_nearest<BVH>(S, l, nudged, L, dist);
-            RT_ACC(5, ts0);
             seelight = (ln >= dist) ? 1.0 : 0.0;
             em.shadow(1);
+#endif
         }
         color = add(color, mul(mul(diff, lv), seelight));
         if (m.flags & SRT_MF_ROUGH) {
@@ -1030,16 +1058,6 @@ RT_HD int sky_collider(const srt_collider* col, int n, const srt_material* mat) 
             k = i;
         }
     return k;
-}
-
-// A texel's 4 bytes as one word (texel_rgb's layouts): one dword load for RGBX / RGBA texels
-RT_HD uint32_t texel_word(const RT_RO srt_texture& T, const RT_RO uint8_t* px) {
-    if (T.channels == 4 && T.channel0 == 0) return *reinterpret_cast<const RT_RO uint32_t*>(px);
-    return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
-}
-RT_HD d3 word_rgb(const SceneView& S, int tid, uint32_t w) {
-    return d3{tex_lut(S, tid, (uint8_t)(w & 0xFFu)), tex_lut(S, tid, (uint8_t)((w >> 8) & 0xFFu)),
-              tex_lut(S, tid, (uint8_t)((w >> 16) & 0xFFu))};
 }
 
 // shade_sky in two halves around the waterfall of the other colliders (trace_one): the texel words
