@@ -1876,13 +1876,17 @@ int mt_ensure(srt_ctx* c) {
     if (c->mt) return SRT_OK;
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_jump),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)MT_LDS_BYTES));
-    HIP_TRY(dalloc(&c->mt, MT_NTAB + 4 * rtmt::N));
+    // jump tables | two round keys | two final windows | the end window's accumulator + its counter
+    HIP_TRY(dalloc(&c->mt, MT_NTAB + 5 * rtmt::N + 1));
     HIP_TRY(hipMemcpy(c->mt, rtmt::tables_flat(), MT_NTAB * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(c->mt + MT_NTAB + 4 * rtmt::N, 0, (rtmt::N + 1) * 4));
     HIP_TRY(dalloc(&c->mt_y, (int64_t)3 * MT_YBLOCKS * rtmt::N));
     return SRT_OK;
 }
 
 uint32_t* mt_dump_at(srt_ctx* c, int d) { return c->mt + MT_NTAB + (2 + d) * rtmt::N; }
+uint32_t* mt_end_acc(srt_ctx* c) { return c->mt + MT_NTAB + 4 * rtmt::N; }
+uint32_t* mt_end_cnt(srt_ctx* c) { return c->mt + MT_NTAB + 5 * rtmt::N; }
 uint32_t* mt_ybuf(srt_ctx* c, int i) { return c->mt_y + (int64_t)i * MT_YBLOCKS * rtmt::N; }
 
 // The y words of `key` for a generation on `st`: those an end block made with the key (a final
@@ -2029,7 +2033,11 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     A.compact = 1;  // the shard's own layout (srt_render reads it by local pixel)
     A.y = mt_y_for(c, st, key);
     A.y_next = mt_ybuf(c, c->mt_cur ^ 1);
-    hipLaunchKernelGGL(k_mt_jump, dim3(T.nseg + 1), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
+    A.end_acc = mt_end_acc(c);
+    A.end_cnt = mt_end_cnt(c);
+    // the segment windows are XOR-accumulated by their jump parts
+    HIP_TRY(hipMemsetAsync(win + rtmt::N, 0, (size_t)T.nseg * rtmt::N * 4, st));
+    hipLaunchKernelGGL(k_mt_jump, dim3((T.nseg + 1) * MT_JUMP_PARTS), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
     HIP_TRY(hipGetLastError());
     if (key_ready) HIP_TRY(hipEventRecord(key_ready, st));
     MtArgs G = A;
@@ -2087,7 +2095,12 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
         }
         if (jump_blocks > 0) {
             A.y = mt_y_for(c, st, A.key);
-            hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
+            A.end_acc = mt_end_acc(c);
+            A.end_cnt = mt_end_cnt(c);
+            // the segment windows are XOR-accumulated by their jump parts
+            if (R.nseg > 1) HIP_TRY(hipMemsetAsync(win + rtmt::N, 0, (size_t)(R.nseg - 1) * rtmt::N * 4, st));
+            hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks * MT_JUMP_PARTS), dim3(MT_THREADS), MT_LDS_BYTES, st, A,
+                               win);
             HIP_TRY(hipGetLastError());
         }
         if (end && key_ready) HIP_TRY(hipEventRecord(key_ready, st));

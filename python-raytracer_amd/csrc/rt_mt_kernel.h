@@ -42,6 +42,12 @@ struct MtArgs {
     // (a shard stores 1/N of the frame's jitter).  Null: the tabulated 2^19-word segments.
     const int64_t* bands;
     int64_t band_len, band_period;
+    // jump parts: each window (a segment's, the end window) is made by MT_JUMP_PARTS blocks, each
+    // XOR-ing 1/MT_JUMP_PARTS of the polynomial's terms into it with atomics (the segment windows are
+    // zeroed before the launch); the end window accumulates in end_acc, and the end part that
+    // arrives last (end_cnt) generates on from it
+    uint32_t* end_acc;  // [624], zero between generations (the last end part leaves it so)
+    uint32_t* end_cnt;  // zero between generations
 };
 
 // Launches per round (k_mt_y only when no earlier end block made the key's y).
@@ -68,12 +74,15 @@ constexpr int MT_THREADS = MT_THREADS_OVERRIDE;
 #else
 constexpr int MT_THREADS = 512;
 #endif
+// blocks per jump (1/MT_JUMP_PARTS of the coefficient words each): a whole jump on one block took
+// ~110 us of a CU; the frame-to-frame chain (each frame's key is the previous frame's end window)
+// waited for the slowest block of the jump kernel
+constexpr int MT_JUMP_PARTS = 8;
 constexpr int MT_WAVES = MT_THREADS / 64;
-constexpr int MT_CW_PER_WAVE = rtmt::N / MT_WAVES;  // 78 coefficient words (8 waves)
 constexpr int MT_G = 11;  // window outputs per lane in the jump (odd: conflict-free LDS reads; 57 lanes cover 624)
 constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
 constexpr int MT_RED = 704;                           // per-wave stride of the reduction buffer (64 x 11)
-static_assert(MT_CW_PER_WAVE * MT_WAVES == rtmt::N, "coefficient words split evenly over the waves");
+static_assert(rtmt::N / MT_JUMP_PARTS / MT_WAVES + 1 <= 64, "a wave's coefficient words fit one per lane");
 static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 32 + MT_G <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
 static_assert(MT_WAVES * MT_RED + 3 * rtmt::N <= MT_YBLOCKS * rtmt::N, "the reduction and end ring alias y");
 constexpr size_t MT_LDS_BYTES = (size_t)MT_YBLOCKS * rtmt::N * 4;  // y
@@ -176,21 +185,26 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_y(const uint32_t* key, uint32
     }
 }
 
-// Tabulated mode: block s - 1 of the grid makes the window of segment s >= 1 into win + 624 s.  Band
-// mode (A.bands): block s makes segment s's window into win + 624 (s + 1) (none for a band at the
-// call's first double: it starts from the key).  With A.end_poly the last block instead jumps to the
-// window at A.end_at and generates forward to the final window (A.dump_at), written to A.dump_dst --
-// the next frame's key, ready when this kernel ends (its whole generation need not have run) -- and
-// on to the y of that window (A.y_next), so the next frame's jump blocks need no k_mt_y.  Block 0
-// also copies the key window to win[0] for the generators that start from it.
+// Jump units, MT_JUMP_PARTS blocks each (block b: unit b / PARTS, part b % PARTS).  Tabulated mode:
+// unit s - 1 makes the window of segment s >= 1 into win + 624 s.  Band mode (A.bands): unit s makes
+// segment s's window into win + 624 (s + 1) (none for a band at the call's first double: it starts
+// from the key).  The windows are XOR-accumulated by their parts with atomics into the zeroed table.
+// With A.end_poly the last unit instead jumps to the window at A.end_at (into A.end_acc), and its part
+// that arrives last generates forward to the final window (A.dump_at), written to A.dump_dst -- the
+// next frame's key, ready when this kernel ends (its whole generation need not have run) -- and on
+// to the y of that window (A.y_next), so the next frame's jump blocks need no k_mt_y.  Block 0 also
+// copies the key window to win[0] for the generators that start from it.
 __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win) {
     extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words
+    __shared__ int last_part;
     uint32_t* y = mt_lds;
     uint32_t* red = mt_lds;                   // MT_WAVES x MT_RED (aliases y once it is read)
-    uint32_t* ring = mt_lds + MT_WAVES * MT_RED;  // end block: 3 blocks after the reduction
-    const bool end_block = A.end_poly && blockIdx.x == gridDim.x - 1;
+    uint32_t* ring = mt_lds + MT_WAVES * MT_RED;  // end unit: 3 blocks after the reduction
+    const int unit = (int)blockIdx.x / MT_JUMP_PARTS, part = (int)blockIdx.x % MT_JUMP_PARTS;
+    const int nunits = (int)gridDim.x / MT_JUMP_PARTS;
+    const bool end_block = A.end_poly && unit == nunits - 1;
     const bool band = A.bands != nullptr;
-    const int s = band ? (int)blockIdx.x : (int)blockIdx.x + 1;
+    const int s = band ? unit : unit + 1;
     const int t = threadIdx.x;
     if (blockIdx.x == 0)
         for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
@@ -205,23 +219,19 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     }
     __syncthreads();
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6), g = t & 63;
+    // this wave's coefficient words: part `part` of the 624, split over the waves
+    const int p_lo = part * rtmt::N / MT_JUMP_PARTS, p_n = (part + 1) * rtmt::N / MT_JUMP_PARTS - p_lo;
+    const int cw_lo = p_lo + wv * p_n / MT_WAVES, cw_n = p_lo + (wv + 1) * p_n / MT_WAVES - cw_lo;
     uint32_t acc[MT_G];
 #pragma unroll
     for (int k = 0; k < MT_G; ++k) acc[k] = 0u;
     // per coefficient word: the lane's 43 words y[32 cw_i + 11 g + i] from LDS, then every set bit j
-    // adds y[32 cw_i + j + 11 g + k] to the lane's eleven outputs k.  The wave's 39 coefficient words
+    // adds y[32 cw_i + j + 11 g + k] to the lane's eleven outputs k.  The wave's coefficient words
     // are held one per lane and read out by v_readlane.
-    uint32_t my_cw[(MT_CW_PER_WAVE + 63) / 64];
-#pragma unroll
-    for (int h = 0; h < (MT_CW_PER_WAVE + 63) / 64; ++h)
-        my_cw[h] = 64 * h + g < MT_CW_PER_WAVE ? poly[wv * MT_CW_PER_WAVE + 64 * h + g] : 0u;
-#ifdef MT_DBG_CW  // (timing harness only: fewer coefficient words per wave)
-    for (int ci = 0; ci < MT_DBG_CW; ++ci) {
-#else
-    for (int ci = 0; ci < MT_CW_PER_WAVE; ++ci) {
-#endif
-        const int cw_i = wv * MT_CW_PER_WAVE + ci;
-        const uint32_t cw = __builtin_amdgcn_readlane(my_cw[ci >> 6], ci & 63);
+    const uint32_t my_cw = g < cw_n ? poly[cw_lo + g] : 0u;
+    for (int ci = 0; ci < cw_n; ++ci) {
+        const int cw_i = cw_lo + ci;
+        const uint32_t cw = __builtin_amdgcn_readlane(my_cw, ci);
         if (cw == 0u) continue;
         // y[32 cw_i + 11 g + i]: single-word loads, the odd lane stride keeps them free of bank conflicts
         const uint32_t* yp = y + 32 * cw_i + MT_G * g;
@@ -254,18 +264,24 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
 #pragma unroll
     for (int k = 0; k < MT_G; ++k) red[wv * MT_RED + MT_G * g + k] = acc[k];
     __syncthreads();
-    uint32_t* wdst = win + (int64_t)(band ? s + 1 : s) * rtmt::N;
+    uint32_t* wdst = end_block ? A.end_acc : win + (int64_t)(band ? s + 1 : s) * rtmt::N;
     for (int m = t; m < rtmt::N; m += MT_THREADS) {
         uint32_t w = 0u;
 #pragma unroll
         for (int v = 0; v < MT_WAVES; ++v) w ^= red[v * MT_RED + m];
-        if (end_block)
-            ring[m] = w;
-        else
-            wdst[m] = w;
+        if (w) atomicXor(wdst + m, w);
     }
     if (!end_block) return;
-    // end block: generate from the window at end_at until the final window (and its y) is written
+    // end unit: the part that arrives last generates from the window at end_at until the final
+    // window (and its y) is written, and leaves the accumulator and the counter zero
+    __threadfence();
+    __syncthreads();
+    if (t == 0) last_part = atomicAdd(A.end_cnt, 1u) == (uint32_t)(MT_JUMP_PARTS - 1);
+    __syncthreads();
+    if (!last_part) return;
+    __threadfence();
+    for (int m = t; m < rtmt::N; m += MT_THREADS) ring[m] = atomicExch(A.end_acc + m, 0u);
+    if (t == 0) atomicExch(A.end_cnt, 0u);
     __syncthreads();
     const int64_t stop = A.dump_at + (A.y_next ? (int64_t)MT_YBLOCKS * rtmt::N : (int64_t)rtmt::N);
     int slot = 0;

@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     }
     const int64_t n_words = 2 * (bands[4 * nb - 4] + band) + 4000;
     std::vector<uint32_t> endp = rtmt::xpow_mod(rtmt::end_jump(n_words));
-    uint32_t *dkey, *dy, *dyn, *dwin, *dpoly, *dend, *ddump;
+    uint32_t *dkey, *dy, *dyn, *dwin, *dpoly, *dend, *ddump, *dacc;
     int64_t* dbands;
     double* dout;
     CK(hipMalloc(&dkey, rtmt::N * 4));
@@ -71,6 +71,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dpoly, polys.size() * 4));
     CK(hipMalloc(&dend, rtmt::N * 4));
     CK(hipMalloc(&ddump, rtmt::N * 4));
+    CK(hipMalloc(&dacc, (rtmt::N + 1) * 4));  // end accumulator + counter (zero between uses)
+    CK(hipMemset(dacc, 0, (rtmt::N + 1) * 4));
     CK(hipMalloc(&dbands, bands.size() * 8));
     CK(hipMalloc(&dout, (size_t)(n_words / 2 + 1) * 8));
     CK(hipMemcpy(dkey, key.data(), rtmt::N * 4, hipMemcpyHostToDevice));
@@ -93,24 +95,28 @@ int main(int argc, char** argv) {
     A.dump_at = ((abs_end + rtmt::N - 1) / rtmt::N - 1) * rtmt::N;
     A.end_at = (int64_t)rtmt::end_jump(n_words);
     A.dump_dst = ddump;
+    A.end_acc = dacc;
+    A.end_cnt = dacc + rtmt::N;
+    const int P = MT_JUMP_PARTS;
     float t_y = time_ms([&] { hipLaunchKernelGGL(k_mt_y, dim3(1), dim3(MT_THREADS), 0, 0, (const uint32_t*)dkey, dy); });
-    float t_j = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(nb), dim3(MT_THREADS), MT_LDS_BYTES, 0, A, dwin); });
+    float t_j = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), MT_LDS_BYTES, 0, A, dwin); });
     MtArgs E = A;
     E.end_poly = dend;
     E.y_next = dyn;
-    float t_je = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(nb + 1), dim3(MT_THREADS), MT_LDS_BYTES, 0, E, dwin); });
+    float t_je = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3((nb + 1) * P), dim3(MT_THREADS), MT_LDS_BYTES, 0, E, dwin); });
     MtArgs E1 = E;
-    E1.bands = nullptr;  // grid 1: only the end block (no band segments)
-    float t_e = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(1), dim3(MT_THREADS), MT_LDS_BYTES, 0, E1, dwin); });
+    E1.bands = nullptr;  // one unit: only the end window (no band segments)
+    float t_e = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(MT_THREADS), MT_LDS_BYTES, 0, E1, dwin); });
     MtArgs E2 = E1;
     E2.y_next = nullptr;
-    float t_e2 = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(1), dim3(MT_THREADS), MT_LDS_BYTES, 0, E2, dwin); });
+    float t_e2 = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(MT_THREADS), MT_LDS_BYTES, 0, E2, dwin); });
     MtArgs G = A;
     G.dump_dst = nullptr;
     float t_g = time_ms(
         [&] { hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(nb), dim3(MT_GEN_THREADS), 0, 0, G, (const uint32_t*)dwin); });
-    // check band 0's window against the serial jump
-    hipLaunchKernelGGL(k_mt_jump, dim3(nb), dim3(MT_THREADS), MT_LDS_BYTES, 0, A, dwin);
+    // check band 0's window against the serial jump (windows are XOR-accumulated: zero them first)
+    CK(hipMemset(dwin + rtmt::N, 0, (size_t)nb * rtmt::N * 4));
+    hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), MT_LDS_BYTES, 0, A, dwin);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> w(rtmt::N), ref(rtmt::N);
     CK(hipMemcpy(w.data(), dwin + rtmt::N, rtmt::N * 4, hipMemcpyDeviceToHost));
