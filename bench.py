@@ -481,8 +481,8 @@ def run_group(args, gpus):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
     ap.add_argument("--rng", default="mt", choices=["mt", "device"],
                     help="mt: the reference's numpy stream generated on the GPU inside every step; device: Philox")

@@ -78,6 +78,15 @@ constexpr uint32_t ERR_INDEX = 1u;      // texture/table index outside the array
 constexpr uint32_t ERR_UNSUPPORTED = 2u;  // uv of a Triangle (undefined in the reference)
 constexpr uint32_t ERR_NAME = 4u;         // a PointLight met by a Glossy hit (NameError in the reference)
 
+// Feature masks of the kernel variants: a kernel instantiated for MATS contains only these shading
+// paths and scene features (the host picks the first variant covering the scene).
+constexpr uint32_t MAT_ALL = 0x3Fu;   // every material type (1 << SRT_GLOSSY .. 1 << SRT_SKY)
+constexpr uint32_t MAT_BVH = 0x40u;   // a triangle BVH (the traversal code)
+constexpr uint32_t MAT_TRI = 0x80u;   // Triangle colliders intersected one by one (collider loops)
+constexpr uint32_t MAT_NMAP = 0x100u; // a normal-mapped material (shading_normal's texel path)
+constexpr uint32_t MAT_GENERIC = MAT_ALL | MAT_TRI | MAT_NMAP;
+constexpr uint32_t mat_bit(int type) { return 1u << type; }
+
 struct d3 {
     double x, y, z;
 };
@@ -360,12 +369,16 @@ RT_HD double triangle_hit(const RT_RO double* p, d3 O, d3 D, double& o) {
     return FARAWAY;
 }
 
+template <uint32_t FEAT = MAT_GENERIC>
 RT_HD double collider_hit(const RT_RO srt_collider& c, d3 O, d3 D, double& o) {
     switch (c.type) {
         case SRT_SPHERE: return sphere_hit(c.p, O, D, o);
         case SRT_PLANE: return plane_hit(c.p, O, D, o);
         case SRT_CUBOID: return cuboid_hit(c.p, O, D, o);
-        default: return triangle_hit(c.p, O, D, o);
+        default:
+            if (FEAT & MAT_TRI) return triangle_hit(c.p, O, D, o);
+            o = FARAWAY;  // (a variant without MAT_TRI is never picked for a scene with triangles)
+            return FARAWAY;
     }
 }
 
@@ -507,9 +520,10 @@ RT_HD d3 word_rgb(const SceneView& S, int tid, uint32_t w) {
 }
 
 // Material.get_Normal (material.py:18-36): collider normal (or normal map) times orientation
+template <uint32_t FEAT = MAT_GENERIC>
 RT_HD d3 shading_normal(const SceneView& S, const RT_RO srt_collider& c, const RT_RO srt_material& m, d3 P,
                         double orient, uint32_t& err) {
-    if (m.normalmap >= 0) {
+    if ((FEAT & MAT_NMAP) && m.normalmap >= 0) {
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
         const RT_RO srt_texture& T = S.tex[m.normalmap];
@@ -708,8 +722,9 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
 
 // BVH: compile the mesh traversal in (kernels instantiated for scenes without a BVH leave it out:
 // its stack would otherwise cost scratch and registers in every kernel)
-template <bool BVH = true>
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH>
 RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bool& ties) {
+    constexpr bool BVH = (FEAT & MAT_BVH) != 0;
     double best = FARAWAY;
     int id = -1;
     double bo = FARAWAY;
@@ -731,7 +746,7 @@ RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bo
             double dmax = np_max(np_max(fabs(D.x), fabs(D.y)), fabs(D.z));
             if (dmin > 0.0 && best * dmax < 0.5 * dmin) continue;
         }
-        double t = collider_hit(cc, O, D, o);
+        double t = collider_hit<FEAT>(cc, O, D, o);
         if (t != t) nan = true;
         if (t < best) { best = t; id = c; bo = o; ties = false; }
         else if (t == best && id >= 0) ties = true;
@@ -809,8 +824,9 @@ RT_HD Child mkchild(d3 o, d3 d, d3 w, uint32_t medium, uint32_t dfl, uint32_t sl
 // min over the shadowed colliders of the distance along the light direction (glossy.py:53-59)
 // `stop`: the caller only asks whether the result is >= stop (seelight), so the BVH pass may stop
 // at the first shadowing triangle closer than that
-template <bool BVH = true>
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH>
 RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L, double stop) {
+    constexpr bool BVH = (FEAT & MAT_BVH) != 0;
     double best = FARAWAY;
     bool first = true;
     const int nl = BVH ? S.nlin : S.ncol;
@@ -822,7 +838,7 @@ RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L, double st
         if (cc.type == SRT_CUBOID)
             t = cuboid_hit_local(cc.p, O, ld3(S.light_local + ((int64_t)light * S.ncol + c) * 3), o);
         else
-            t = collider_hit(cc, O, L, o);
+            t = collider_hit<FEAT>(cc, O, L, o);
         best = first ? t : np_min(best, t);
         first = false;
     }
@@ -831,13 +847,13 @@ RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L, double st
 }
 
 // Glossy.get_color (glossy.py:25-110)
-template <bool BVH = true, class E>
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH, class E>
 RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, double orient,
                         E& em, uint32_t& err) {
     const RT_RO srt_material& m = S.mat[mi];
     RT_T0(tg0);
     d3 P = add(r.o, mul(r.d, t));
-    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 N = shading_normal<FEAT>(S, c, m, P, orient, err);
     // the texel word of a textured material is loaded first and read after the shadow tests of the
     // lights (which do not depend on it), so its latency overlaps them; the colour is then composed
     // in the reference's order (glossy.py:30-84)
@@ -860,7 +876,7 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
 #ifndef RT_ABL_SHADOW  // (diagnostic build only: time without the shadow test)
         if (S.nshadow > 0) {
             RT_T0(ts0);
-            const double ln = shadow_nearest<BVH>(S, l, nudged, ld3(Lt.dir), SKYBOX_DISTANCE);
+            const double ln = shadow_nearest<FEAT>(S, l, nudged, ld3(Lt.dir), SKYBOX_DISTANCE);
             RT_ACC(5, ts0);
             if (ln >= SKYBOX_DISTANCE) see |= 1u << l;
             em.shadow(1);
@@ -890,7 +906,7 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
             seelight = ((see >> l) & 1u) ? 1.0 : 0.0;
 #ifndef RT_ABL_SHADOW
         } else if (S.nshadow > 0) {
-            double ln = shadow_nearest<BVH>(S, l, nudged, L, dist);
+            double ln = shadow_nearest<FEAT>(S, l, nudged, L, dist);
             seelight = (ln >= dist) ? 1.0 : 0.0;
             em.shadow(1);
 #endif
@@ -934,13 +950,13 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
 }
 
 // Refractive.get_color (refractive.py:24-123); `mc_u` is the uniform for the MC pick
-template <class E>
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH, class E>
 RT_HD void shade_refractive(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t,
                             double orient, E& em, uint32_t& err, double mc_u) {
     if ((int)meta_depth(r.meta) >= c.max_ray_depth) return;  // black beyond max_ray_depth
     const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
-    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 N = shading_normal<FEAT>(S, c, m, P, orient, err);
     d3 V = mul(r.d, -1.0);
     uint32_t m1 = meta_medium(r.meta);
     uint32_t m2 = (orient == 1.0) ? (uint32_t)m.medium : 0u;
@@ -994,13 +1010,13 @@ RT_HD void shade_refractive(const SceneView& S, const RT_RO srt_collider& c, int
 }
 
 // ThinFilmInterference.get_color (thin_film_interference.py:24-115)
-template <class E>
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH, class E>
 RT_HD void shade_thinfilm(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t,
                           double orient, E& em, uint32_t& err) {
     if ((int)meta_depth(r.meta) >= c.max_ray_depth) return;
     const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
-    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 N = shading_normal<FEAT>(S, c, m, P, orient, err);
     d3 V = mul(r.d, -1.0);
     double cos_i = dot(V, N);
     const RT_RO srt_texture& lut = S.tex[m.tex_aux0];
@@ -1101,14 +1117,14 @@ RT_HD void shade_emissive(const SceneView& S, const RT_RO srt_collider& c, int m
 }
 
 // Diffuse.get_color (diffuse.py:25-124): no local colour; the children carry the estimate
-template <class E>
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH, class E>
 RT_HD void shade_diffuse(const SceneView& S, const RT_RO srt_collider& c, int mi, const Ray& r, double t, double orient,
                          E& em, uint32_t& err) {
     uint32_t dfl = meta_diffuse(r.meta);
     if (dfl >= 2) return;
     const RT_RO srt_material& m = S.mat[mi];
     d3 P = add(r.o, mul(r.d, t));
-    d3 N = shading_normal(S, c, m, P, orient, err);
+    d3 N = shading_normal<FEAT>(S, c, m, P, orient, err);
     d3 diff;
     if (m.tex >= 0) {
         double u, v;
@@ -1190,29 +1206,24 @@ RT_HD Child diffuse_child(const SceneView& S, const RT_RO srt_material& m, const
     return mkchild(g.P, dir, mul(g.w, ndl / pdf), g.medium, g.dfl, 0x100u + k);
 }
 
-// Material-type bit masks: a kernel instantiated for MATS contains only those shading paths.
-constexpr uint32_t MAT_ALL = 0x3Fu;
-// not a material: the scene has a triangle BVH (kernels without this bit carry no traversal code)
-constexpr uint32_t MAT_BVH = 0x40u;
-constexpr uint32_t mat_bit(int type) { return 1u << type; }
 
 // Shade one (ray, collider) hit with a per-lane (possibly divergent) material.
-template <uint32_t MATS = MAT_ALL, class E>
+template <uint32_t MATS = MAT_GENERIC | MAT_BVH, class E>
 RT_HD void shade_hit(const SceneView& S, int cid, int mi, const Ray& r, double t, double orient, E& em,
                      uint32_t& err, double mc_u) {
     const RT_RO srt_collider& c = S.col[cid];
     switch (S.mat[mi].type) {
         case SRT_GLOSSY:
-            if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<(MATS & MAT_BVH) != 0>(S, c, mi, r, t, orient, em, err);
+            if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<MATS>(S, c, mi, r, t, orient, em, err);
             break;
         case SRT_REFRACTIVE:
-            if (MATS & mat_bit(SRT_REFRACTIVE)) shade_refractive(S, c, mi, r, t, orient, em, err, mc_u);
+            if (MATS & mat_bit(SRT_REFRACTIVE)) shade_refractive<MATS>(S, c, mi, r, t, orient, em, err, mc_u);
             break;
         case SRT_THINFILM:
-            if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, mi, r, t, orient, em, err);
+            if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm<MATS>(S, c, mi, r, t, orient, em, err);
             break;
         case SRT_DIFFUSE:
-            if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse(S, c, mi, r, t, orient, em, err);
+            if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse<MATS>(S, c, mi, r, t, orient, em, err);
             break;
         case SRT_EMISSIVE:
             if (MATS & mat_bit(SRT_EMISSIVE)) shade_emissive(S, c, mi, r, t, em, err);

@@ -124,14 +124,14 @@ void trace_one(const SceneView& S, const Ray& r, int depth, uint64_t seed, std::
     if (hit_slot) *hit_slot = id;
     if (id < 0) return;
     HostEmit em{S, r, next, fb, npix, seed, depth, 0u, &shadow};
-    shade_hit<MAT_ALL | MAT_BVH>(S, id, S.col[id].material, r, t, o, em, err, mc_uniform(S, seed, depth, r, id, 0));
+    shade_hit<MAT_GENERIC | MAT_BVH>(S, id, S.col[id].material, r, t, o, em, err, mc_uniform(S, seed, depth, r, id, 0));
     if (ties) {
         uint32_t round = 1;
         for (int c = id + 1; c < S.ncol; ++c) {
             double oc;
             if (collider_hit(S.col[c], r.o, r.d, oc) == t) {
                 HostEmit et{S, r, next, fb, npix, seed, depth, round, &shadow};
-                shade_hit<MAT_ALL | MAT_BVH>(S, c, S.col[c].material, r, t, oc, et, err,
+                shade_hit<MAT_GENERIC | MAT_BVH>(S, c, S.col[c].material, r, t, oc, et, err,
                                              mc_uniform(S, seed, depth, r, c, round));
                 ++round;
             }

@@ -492,7 +492,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
             }
         }
     } else if (active) {
-        id = nearest_hit<(MATS & MAT_BVH) != 0>(S, r.o, r.d, t, o, ties);
+        id = nearest_hit<MATS>(S, r.o, r.d, t, o, ties);
     }
     if constexpr (em_in_place<Em>::value) {
         // the emitter writes the child over `r` (the fused path): no tie loop, which would read the
@@ -544,17 +544,17 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
             if (rnd) em.round = rnd;
             switch (S.mat[m].type) {
                 case SRT_GLOSSY:
-                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<(MATS & MAT_BVH) != 0>(S, c, m, r, t, co, em, err);
+                    if (MATS & mat_bit(SRT_GLOSSY)) shade_glossy<MATS>(S, c, m, r, t, co, em, err);
                     break;
                 case SRT_REFRACTIVE:
                     if (MATS & mat_bit(SRT_REFRACTIVE))
-                        shade_refractive(S, c, m, r, t, co, em, err, mc_uniform(P, r, cs, rnd));
+                        shade_refractive<MATS>(S, c, m, r, t, co, em, err, mc_uniform(P, r, cs, rnd));
                     break;
                 case SRT_THINFILM:
-                    if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm(S, c, m, r, t, co, em, err);
+                    if (MATS & mat_bit(SRT_THINFILM)) shade_thinfilm<MATS>(S, c, m, r, t, co, em, err);
                     break;
                 case SRT_DIFFUSE:
-                    if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse(S, c, m, r, t, co, em, err);
+                    if (MATS & mat_bit(SRT_DIFFUSE)) shade_diffuse<MATS>(S, c, m, r, t, co, em, err);
                     break;
                 case SRT_EMISSIVE:
                     if (MATS & mat_bit(SRT_EMISSIVE)) shade_emissive(S, c, m, r, t, em, err);
@@ -571,7 +571,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
             double no = FARAWAY;
             for (int c = cu + 1; c < S.ncol; ++c) {
                 double oc;
-                if (mine && ties && nxt < 0 && collider_hit(S.col[c], r.o, r.d, oc) == t) {
+                if (mine && ties && nxt < 0 && collider_hit<MATS>(S.col[c], r.o, r.d, oc) == t) {
                     nxt = c;
                     no = oc;
                 }
@@ -1200,10 +1200,11 @@ const Variant VARIANTS[] = {
     {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
     {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
-    {MAT_ALL, k_primary<MAT_ALL, OCC>, k_trace<MAT_ALL, OCC>, k_frame<MAT_ALL, OCC>, k_trace<MAT_ALL, OCC, true>},
+    {MAT_GENERIC, k_primary<MAT_GENERIC, OCC>, k_trace<MAT_GENERIC, OCC>, k_frame<MAT_GENERIC, OCC>,
+     k_trace<MAT_GENERIC, OCC, true>},
     // scenes with a triangle BVH (TriangleMesh)
-    {MAT_ALL | MAT_BVH, k_primary<MAT_ALL | MAT_BVH, OCC>, k_trace<MAT_ALL | MAT_BVH, OCC>, k_frame<MAT_ALL | MAT_BVH, OCC>,
-     k_trace<MAT_ALL | MAT_BVH, OCC, true>},
+    {MAT_GENERIC | MAT_BVH, k_primary<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC>,
+     k_frame<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC, true>},
 };
 const Variant& pick_variant(uint32_t mats) {
 #ifdef RT_OCC_VARIANTS
@@ -1666,6 +1667,7 @@ struct srt_ctx {
     // rounds of threads: ex1 1080p 1.308 -> 1.209 ms per frame, a rank of 4 0.47 -> 0.44, while a rank
     // of 8 (1.3 rounds) is faster per depth, 0.29 vs 0.35 (profiles/r03_fused_ab.txt)
     int fuse_primary = -1;
+    int pix_groups_opt = 0;     // option "pix_groups": k_primary's sample groups per pixel (power of two; 0 auto)
     double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
@@ -1815,6 +1817,7 @@ int64_t fused_items(const srt_ctx* c) { return 2 * (int64_t)c->ncu * 4 * OCC * 6
 // k_primary's sample groups per pixel (TraceParams::pix_groups): the fewest (a power of two, at most
 // the pass's samples and 64) that give the pass enough threads
 int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
+    if (c->pix_groups_opt > 0) return std::min(c->pix_groups_opt, 64);  // (option "pix_groups": experiments)
     const int64_t want = fused ? fused_items(c) : (int64_t)c->max_blocks * 64;
     int g = 1;
     while (g * 2 <= std::min(ns, 64) && npix * g < want) g *= 2;
@@ -2428,6 +2431,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     }
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "fuse_primary")) { c->fuse_primary = (int)value; return SRT_OK; }
+    if (!strcmp(key, "pix_groups")) {
+        if (value < 0 || value > 64 || (value & (value - 1))) return fail(SRT_ERR_ARG, "pix_groups: 0 (auto) or 1, 2, 4 .. 64");
+        c->pix_groups_opt = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
     if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
     if (!strcmp(key, "deterministic")) {
@@ -2603,9 +2611,11 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     S.nmedia = d->n_media; S.nimp = d->n_importance;
     S.sky_col = c->sky_prefetch ? sky_collider(d->colliders, d->n_colliders, d->materials) : -1;
     S.nshadow = 0;
+    bool lin_tri = false;
     {
         // triangle meshes: BVH over the Triangle colliders, the rest intersected one by one
         BvhBuild B;
+        lin_tri = false;
         if (c->use_bvh) {
             bvh_build(d->colliders, d->n_colliders, B);
         } else {
@@ -2621,6 +2631,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
         S.bvh_tri = (decltype(S.bvh_tri))tri;
         S.bvh = (decltype(S.bvh))nodes;
         S.bvh_nodes = (int)B.nodes.size();
+        for (int k : B.lin) lin_tri |= d->colliders[k].type == SRT_TRIANGLE;
     }
     int fan = 1;
     c->has_diffuse = 0;
@@ -2640,6 +2651,9 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     c->mats = 0;
     for (int i = 0; i < d->n_materials; ++i) c->mats |= mat_bit(d->materials[i].type);
     if (S.bvh_nodes > 0) c->mats |= MAT_BVH;
+    if (lin_tri) c->mats |= MAT_TRI;  // Triangle colliders outside the BVH
+    for (int i = 0; i < d->n_materials; ++i)
+        if (d->materials[i].normalmap >= 0) c->mats |= MAT_NMAP;
     c->chain_ok = true;
     c->hint_key[0] = -1;  // ray counts of another scene are no plan for this one
     c->has_scene = true;
@@ -3324,7 +3338,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
                 P.force_id = dfid;
                 P.force_t = dft;
                 P.force_o = dfo;
-                hipLaunchKernelGGL((c->mats & MAT_BVH) ? k_shade_forced<MAT_ALL | MAT_BVH> : k_shade_forced<MAT_ALL>,
+                hipLaunchKernelGGL((c->mats & MAT_BVH) ? k_shade_forced<MAT_GENERIC | MAT_BVH> : k_shade_forced<MAT_GENERIC>,
                                    dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream, P);
                 P.force_id = nullptr;
                 P.force_t = P.force_o = nullptr;
