@@ -482,7 +482,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
     ap.add_argument("--rng", default="mt", choices=["mt", "device"],
                     help="mt: the reference's numpy stream generated on the GPU inside every step; device: Philox")
@@ -492,6 +492,8 @@ def main():
     ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
     ap.add_argument("--option", action="append", default=[],
                     help="experiment: srt_set_option KEY=VALUE before rendering (repeatable)")
+    ap.add_argument("--device-outputs", action="store_true",
+                    help="diagnostic (one process): the frames' outputs left in HBM instead of host memory")
     ap.add_argument("--sync", action="store_true",
                     help="diagnostic: synchronous timed frames (no pipelining), so a rocprofv3 kernel trace shows each "
                          "kernel's launch time alone, as the roofline's HIP-event kernel_ms measures it")
@@ -577,6 +579,11 @@ def main():
     outs = []
     for k in range(NOUT):
         pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
+        if args.device_outputs and world == 1:  # (diagnostic: no host copies)
+            N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full, ctypes.byref(pu)))
+            N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full * 8, ctypes.byref(pr)))
+            outs.append((pu, pr))
+            continue
         if rank == 0:
             N.check(lib, lib.srt_host_alloc(ctx, 3 * npix_full, ctypes.byref(pu)))
         if world > 1:
@@ -613,12 +620,20 @@ def main():
             N.check(lib, lib.srt_comm_barrier(ctx))
 
     rank_ms, rank_rays, enq = [], [], []
-    for rr, rows_r in rehearse.items():
+    for i, (rr, rows_r) in enumerate(rehearse.items()):
         if rows_r is not None:
             rows32 = rows_r
             a.rows, a.n_rows = N.ptr(rows32), len(rows32)
-        for w in range(args.warmup):
+        t_w = time.perf_counter()
+        w = 0
+        # rehearsing several ranks: the first one's warm-up also runs >= 0.5 s of frames, so that it
+        # does not carry the GPU's own warm-up into the slowest-rank figure
+        prime_s = 0.5 if (i == 0 and len(rehearse) > 1) else 0.0
+        while w < args.warmup or time.perf_counter() - t_w < prime_s:
             step(async_ok=w > 0)  # the first frame runs synchronously (sizes queues and rings)
+            w += 1
+            if w % 50 == 0:
+                barrier()  # (bounded queue depth while priming)
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):

@@ -9,8 +9,10 @@
 //
 // Build: a binary BVH by binned SAH (16 bins on the longest centroid axis), leaves of at most 4
 // triangles, depth capped at BVH_MAX_DEPTH; then collapsed into 4-wide nodes (rt_device.h BvhNode):
-// a node's slots start as its two children, and the slot of largest surface area that is an inner
-// node is replaced by its two children while fewer than four slots are taken.  Boxes are the
+// a node's slots are its grandchildren (a leaf child stands for itself), so every 4-wide level spans
+// two binary levels and the traversal stack stays within BVH_STACK.  Leaves keep < 64 triangles and
+// their slots < 2^25 (the traversal's child codes); a mesh beyond that (a depth-capped leaf of 64 or
+// more triangles) stays in the linear collider loop.  Boxes are the
 // triangles' vertex boxes inflated by 1e-9 * (1 + max |coordinate|) -- the reference intersects the
 // plane through the centroid and tests edge half-spaces with >= 0, so a hit point may sit a few ulps
 // outside the vertex box -- then rounded outward to float.
@@ -26,8 +28,10 @@ namespace rt {
 
 constexpr int BVH_MIN_TRIANGLES = 8;  // fewer triangles stay in the linear collider loop
 constexpr int BVH_LEAF = 4;
-constexpr int BVH_MAX_DEPTH = 20;  // binary levels (so at most 20 4-wide levels: 61 stack entries <= BVH_STACK)
-static_assert(3 * BVH_MAX_DEPTH + 1 <= BVH_STACK, "traversal stack holds the deepest path");
+constexpr int BVH_MAX_DEPTH = 20;  // binary levels (so at most 10 4-wide levels: 31 stack entries <= BVH_STACK)
+static_assert(3 * ((BVH_MAX_DEPTH + 1) / 2) + 1 <= BVH_STACK, "traversal stack holds the deepest path");
+constexpr int BVH_LEAF_MAX = 63;            // triangles per leaf (6-bit count in the child code)
+constexpr int32_t BVH_SLOTS_MAX = 1 << 25;  // leaf slots (first << 6 fits the child code)
 
 struct BvhBuild {
     std::vector<BvhNode> nodes;
@@ -210,20 +214,15 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
     while (!work.empty()) {
         const auto [bn, wn] = work.back();
         work.pop_back();
-        std::vector<int> slots{bin[bn].first, bin[bn].first + 1};
-        while (slots.size() < 4) {
-            int pick = -1;
-            double pa = -1.0;
-            for (size_t k = 0; k < slots.size(); ++k) {
-                const BinNode& c = bin[slots[k]];
-                if (c.count > 0 || c.first < 0) continue;
-                const double a = area(c.lo, c.hi);
-                if (a > pa) { pa = a; pick = (int)k; }
+        std::vector<int> slots;
+        for (int h = 0; h < 2; ++h) {
+            const BinNode& c = bin[bin[bn].first + h];
+            if (c.count > 0 || c.first < 0) {
+                slots.push_back(bin[bn].first + h);
+            } else {
+                slots.push_back(c.first);
+                slots.push_back(c.first + 1);
             }
-            if (pick < 0) break;
-            const int f = bin[slots[pick]].first;
-            slots[pick] = f;
-            slots.insert(slots.begin() + pick + 1, f + 1);
         }
         BvhNode nd4{};
         for (int k = 0; k < 4; ++k) {
@@ -253,6 +252,14 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
         }
         out.nodes[wn] = nd4;
     }
+    for (const BinNode& b : bin)
+        if (b.count > BVH_LEAF_MAX || (b.count > 0 && b.first + b.count > BVH_SLOTS_MAX)) {
+            out.nodes.clear();
+            out.tri.clear();
+            out.lin.clear();
+            for (int i = 0; i < n; ++i) out.lin.push_back(i);
+            return;
+        }
 }
 
 }  // namespace rt

@@ -14,6 +14,7 @@
 #include <math.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/sightpy_rt.h"
 
@@ -262,7 +263,7 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 128, "one 128-byte line per BVH node");
 constexpr int32_t BVH_EMPTY = (int32_t)0x80000000;
-constexpr int BVH_STACK = 64;  // (3 entries per 4-wide level at most: depth <= 20 levels)
+constexpr int BVH_STACK = 32;  // (3 entries per 4-wide level at most: depth <= 10 levels)
 
 // The kernel's dynamic LDS: the texture tables [0, nlut_lds) staged by the trace kernels first
 // (rt_kernels.hip stage_luts), read directly (no pointer in the scene view, so the kernels' scene view
@@ -635,87 +636,133 @@ RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear)
     return t0 <= t1 && t1 >= 0.0;
 }
 
+// Traversal stack entries, one 64-bit word each: the entry distance as float bits (rounded down: a
+// lower bound, so pruning never drops a box that holds a hit) over a child code -- an inner node's
+// index (>= 0) or a leaf, -(1 + (first << 6 | count)) (rt_bvh.h keeps leaves below 64 triangles and
+// 2^25 slots).  Leaves go on the stack like nodes, so the triangle loop appears once.
+#if defined(__HIPCC__)
+#define RT_UNROLL _Pragma("unroll")
+#else
+#define RT_UNROLL
+#endif
+RT_HD uint32_t bvh_f2u(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __float_as_uint(f);
+#else
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+#endif
+}
+RT_HD float bvh_u2f(uint32_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __uint_as_float(u);
+#else
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+#endif
+}
+RT_HD uint64_t bvh_entry(double tn, int32_t code) {
+    float f = (float)tn;
+    if ((double)f > tn) f = nextafterf(f, -INFINITY);
+    return ((uint64_t)bvh_f2u(f) << 32) | (uint32_t)code;
+}
+RT_HD int32_t bvh_code(int32_t child, int32_t count) {
+    return child >= 0 ? child : -(1 + (((-child - 1) << 6) | count));
+}
+
+// The four children of a node against the ray: entry distances t[k] (INFINITY: missed, empty, or
+// entered beyond `limit`) and child codes c[k], sorted by distance (a sorting network on registers).
+RT_HD void bvh_children(const RT_RO BvhNode& nd, d3 O, d3 inv, double limit, bool strict, double t[4],
+                        int32_t c[4]) {
+RT_UNROLL
+    for (int k = 0; k < 4; ++k) {
+        c[k] = bvh_code(nd.child[k], nd.count[k]);
+        double tn;
+        const bool hit = nd.child[k] != BVH_EMPTY && box4_hit(nd, k, O, inv, tn) && (strict ? tn < limit : tn <= limit);
+        t[k] = hit ? tn : INFINITY;
+    }
+    auto cs = [&](int a, int b) {
+        const bool sw = t[b] < t[a];
+        const double ta = sw ? t[b] : t[a], tb = sw ? t[a] : t[b];
+        const int32_t ca = sw ? c[b] : c[a], cb = sw ? c[a] : c[b];
+        t[a] = ta;
+        t[b] = tb;
+        c[a] = ca;
+        c[b] = cb;
+    };
+    cs(0, 1);
+    cs(2, 3);
+    cs(0, 2);
+    cs(1, 3);
+    cs(1, 2);
+}
+
 // Nearest BVH triangle, merged into (best, id, bo, ties) with the reference's rule independent of
 // visiting order: the smallest distance wins, among equal distances the lowest collider index,
 // and `ties` records that another collider hit at that distance.  Boxes entered beyond `best` are
-// pruned (a box entered exactly at `best` is still visited: it may hold a tie); a node's leaves are
-// tested at once, its inner children pushed farthest first (the nearest is popped next) with their
-// entry distance, which prunes them again on pop.  Triangles never return NaN (a NaN ray fails every
-// comparison of triangle_hit and misses).
+// pruned (a box entered exactly at `best` is still visited: it may hold a tie); a node's hit children
+// are pushed farthest first (the nearest is popped next) with their entry distance, which prunes them
+// again on pop.  Triangles never return NaN (a NaN ray fails every comparison of triangle_hit and
+// misses).
 RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
     const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
-    int stack[BVH_STACK];
-    float stn[BVH_STACK];  // entry distances rounded down (a lower bound: prunes no box that holds a hit)
+    uint64_t stack[BVH_STACK];
     int sp = 0;
-    stack[sp] = 0;
-    stn[sp++] = -INFINITY;
+    stack[sp++] = bvh_entry(-INFINITY, 0);
     while (sp > 0) {
-        --sp;
-        if ((double)stn[sp] > best) continue;
-        const RT_RO BvhNode& nd = S.bvh[stack[sp]];
-        int in[4];
-        double it[4];
-        int ni = 0;
-        for (int k = 0; k < 4; ++k) {
-            const int32_t ch = nd.child[k];
-            double tn;
-            if (ch == BVH_EMPTY || !box4_hit(nd, k, O, inv, tn) || tn > best) continue;
-            if (ch < 0) {
-                for (int j = -ch - 1, e = -ch - 1 + nd.count[k]; j < e; ++j) {
-                    const int c = S.bvh_tri[j];
-                    double o;
-                    const double t = triangle_hit(S.col[c].p, O, D, o);
-                    if (t < best) { best = t; id = c; bo = o; ties = false; }
-                    else if (t == best && best != FARAWAY) {
-                        ties = true;
-                        if (c < id) { id = c; bo = o; }
-                    }
+        const uint64_t e = stack[--sp];
+        if ((double)bvh_u2f((uint32_t)(e >> 32)) > best) continue;
+        const int32_t code = (int32_t)(uint32_t)e;
+        if (code < 0) {
+            const int first = (-code - 1) >> 6, cnt = (-code - 1) & 63;
+            for (int j = first; j < first + cnt; ++j) {
+                const int c = S.bvh_tri[j];
+                double o;
+                const double t = triangle_hit(S.col[c].p, O, D, o);
+                if (t < best) { best = t; id = c; bo = o; ties = false; }
+                else if (t == best && best != FARAWAY) {
+                    ties = true;
+                    if (c < id) { id = c; bo = o; }
                 }
-            } else {
-                // insertion by entry distance, nearest last
-                int j = ni++;
-                while (j > 0 && it[j - 1] < tn) {
-                    in[j] = in[j - 1];
-                    it[j] = it[j - 1];
-                    --j;
-                }
-                in[j] = ch;
-                it[j] = tn;
             }
+            continue;
         }
-        for (int j = 0; j < ni && sp < BVH_STACK; ++j) {
-            float f = (float)it[j];
-            if ((double)f > it[j]) f = nextafterf(f, -INFINITY);
-            stack[sp] = in[j];
-            stn[sp++] = f;
-        }
+        double t[4];
+        int32_t c[4];
+        bvh_children(S.bvh[code], O, inv, best, false, t, c);
+RT_UNROLL
+        for (int k = 3; k >= 0; --k)
+            if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = bvh_entry(t[k], c[k]);
     }
 }
 
 // Any shadowed BVH triangle closer than `stop` along L: returns its distance, else FARAWAY.
 RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
     const d3 inv = d3{1.0 / L.x, 1.0 / L.y, 1.0 / L.z};
-    int stack[BVH_STACK];
+    int32_t stack[BVH_STACK];
     int sp = 0;
     stack[sp++] = 0;
     while (sp > 0) {
-        const RT_RO BvhNode& nd = S.bvh[stack[--sp]];
-        for (int k = 0; k < 4; ++k) {
-            const int32_t ch = nd.child[k];
-            double tn;
-            if (ch == BVH_EMPTY || !box4_hit(nd, k, O, inv, tn) || tn >= stop) continue;
-            if (ch < 0) {
-                for (int j = -ch - 1, e = -ch - 1 + nd.count[k]; j < e; ++j) {
-                    const RT_RO srt_collider& cc = S.col[S.bvh_tri[j]];
-                    if (!(cc.flags & SRT_CF_SHADOW)) continue;
-                    double o;
-                    const double t = triangle_hit(cc.p, O, L, o);
-                    if (t < stop) return t;
-                }
-            } else if (sp < BVH_STACK) {
-                stack[sp++] = ch;
+        const int32_t code = stack[--sp];
+        if (code < 0) {
+            const int first = (-code - 1) >> 6, cnt = (-code - 1) & 63;
+            for (int j = first; j < first + cnt; ++j) {
+                const RT_RO srt_collider& cc = S.col[S.bvh_tri[j]];
+                if (!(cc.flags & SRT_CF_SHADOW)) continue;
+                double o;
+                const double t = triangle_hit(cc.p, O, L, o);
+                if (t < stop) return t;
             }
+            continue;
         }
+        double t[4];
+        int32_t c[4];
+        bvh_children(S.bvh[code], O, inv, stop, true, t, c);
+RT_UNROLL
+        for (int k = 3; k >= 0; --k)
+            if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = c[k];
     }
     return FARAWAY;
 }

@@ -1200,6 +1200,10 @@ const Variant VARIANTS[] = {
     {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
     {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
+    // a glossy TriangleMesh in the ex1 setting (the mesh bench): the BVH traversal, no other features
+    {MATS_GLOSSY_SKY | MAT_BVH, k_primary<MATS_GLOSSY_SKY | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_BVH, OCC>,
+     k_frame<MATS_GLOSSY_SKY | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_BVH, OCC, true>,
+     k_primary<MATS_GLOSSY_SKY | MAT_BVH, RT_FUSE_OCC, true>},
     {MAT_GENERIC, k_primary<MAT_GENERIC, OCC>, k_trace<MAT_GENERIC, OCC>, k_frame<MAT_GENERIC, OCC>,
      k_trace<MAT_GENERIC, OCC, true>},
     // scenes with a triangle BVH (TriangleMesh)
@@ -1576,6 +1580,8 @@ struct srt_ctx {
     bool texels_rgbx = false;  // the resident pool holds 3-channel images as RGBX
     bool texel_rgbx = true;    // option "texel_rgbx": store 3-channel images as RGBX (one dword per texel)
     bool sky_prefetch = true;  // option "sky_prefetch" (next srt_upload_scene): trace_one's early sky texel fetch
+    // option "mt_jump_parts": blocks per jump window (0: mt_jump_parts's choice)
+    int mt_parts_opt = 0;
     // camera tables (shared by the slots; uploaded only when they change)
     double* xs = nullptr;
     double* ys = nullptr;
@@ -1892,6 +1898,9 @@ uint32_t* mt_end_acc(srt_ctx* c) { return c->mt + MT_NTAB + 4 * rtmt::N; }
 uint32_t* mt_end_cnt(srt_ctx* c) { return c->mt + MT_NTAB + 5 * rtmt::N; }
 uint32_t* mt_ybuf(srt_ctx* c, int i) { return c->mt_y + (int64_t)i * MT_YBLOCKS * rtmt::N; }
 
+// Blocks per jump window (k_mt_jump parts): the option, else MT_MAX_PARTS
+int mt_jump_parts(const srt_ctx* c) { return c->mt_parts_opt ? c->mt_parts_opt : MT_MAX_PARTS; }
+
 // The y words of `key` for a generation on `st`: those an end block made with the key (a final
 // window), else k_mt_y into the scratch buffer (one workgroup, ~34 blocks).  Generations of
 // different frames are ordered by the key they hand on, so one scratch buffer suffices.
@@ -2038,9 +2047,11 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     A.y_next = mt_ybuf(c, c->mt_cur ^ 1);
     A.end_acc = mt_end_acc(c);
     A.end_cnt = mt_end_cnt(c);
+    A.parts = mt_jump_parts(c);
     // the segment windows are XOR-accumulated by their jump parts
     HIP_TRY(hipMemsetAsync(win + rtmt::N, 0, (size_t)T.nseg * rtmt::N * 4, st));
-    hipLaunchKernelGGL(k_mt_jump, dim3((T.nseg + 1) * MT_JUMP_PARTS), dim3(MT_THREADS), MT_LDS_BYTES, st, A, win);
+    hipLaunchKernelGGL(k_mt_jump, dim3((T.nseg + 1) * A.parts), dim3(MT_THREADS), mt_jump_lds_bytes(A.parts), st, A,
+                       win);
     HIP_TRY(hipGetLastError());
     if (key_ready) HIP_TRY(hipEventRecord(key_ready, st));
     MtArgs G = A;
@@ -2100,10 +2111,11 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
             A.y = mt_y_for(c, st, A.key);
             A.end_acc = mt_end_acc(c);
             A.end_cnt = mt_end_cnt(c);
+            A.parts = mt_jump_parts(c);
             // the segment windows are XOR-accumulated by their jump parts
             if (R.nseg > 1) HIP_TRY(hipMemsetAsync(win + rtmt::N, 0, (size_t)(R.nseg - 1) * rtmt::N * 4, st));
-            hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks * MT_JUMP_PARTS), dim3(MT_THREADS), MT_LDS_BYTES, st, A,
-                               win);
+            hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks * A.parts), dim3(MT_THREADS), mt_jump_lds_bytes(A.parts),
+                               st, A, win);
             HIP_TRY(hipGetLastError());
         }
         if (end && key_ready) HIP_TRY(hipEventRecord(key_ready, st));
@@ -2415,6 +2427,12 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
     if (!strcmp(key, "texel_rgbx")) { c->texel_rgbx = value != 0; return SRT_OK; }  // (next srt_upload_scene)
     if (!strcmp(key, "sky_prefetch")) { c->sky_prefetch = value != 0; return SRT_OK; }  // (next srt_upload_scene)
+    if (!strcmp(key, "mt_jump_parts")) {
+        if (value != 0 && (value < MT_MIN_PARTS || value > MT_MAX_PARTS))
+            return fail(SRT_ERR_ARG, "mt_jump_parts: 0 (auto) or 2 .. 8");
+        c->mt_parts_opt = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "frame_groups")) {
         if (value < 0 || value > 4096) return fail(SRT_ERR_ARG, "frame_groups: 0 (auto) .. 4096");
         c->frame_groups = (int)value;

@@ -42,12 +42,14 @@ struct MtArgs {
     // (a shard stores 1/N of the frame's jitter).  Null: the tabulated 2^19-word segments.
     const int64_t* bands;
     int64_t band_len, band_period;
-    // jump parts: each window (a segment's, the end window) is made by MT_JUMP_PARTS blocks, each
-    // XOR-ing 1/MT_JUMP_PARTS of the polynomial's terms into it with atomics (the segment windows are
-    // zeroed before the launch); the end window accumulates in end_acc, and the end part that
-    // arrives last (end_cnt) generates on from it
+    // jump parts: each window (a segment's, the end window) is made by `parts` blocks, each XOR-ing
+    // 1/parts of the polynomial's terms into it with atomics (the segment windows are zeroed before
+    // the launch); the end window accumulates in end_acc, and the end part that arrives last
+    // (end_cnt) generates on from it
     uint32_t* end_acc;  // [624], zero between generations (the last end part leaves it so)
     uint32_t* end_cnt;  // zero between generations
+    int32_t parts;      // MT_MIN_PARTS .. MT_MAX_PARTS; the launch's LDS is mt_jump_lds_bytes(parts)
+    int32_t pad_;
 };
 
 // Launches per round (k_mt_y only when no earlier end block made the key's y).
@@ -74,18 +76,27 @@ constexpr int MT_THREADS = MT_THREADS_OVERRIDE;
 #else
 constexpr int MT_THREADS = 512;
 #endif
-// blocks per jump (1/MT_JUMP_PARTS of the coefficient words each): a whole jump on one block took
-// ~110 us of a CU; the frame-to-frame chain (each frame's key is the previous frame's end window)
-// waited for the slowest block of the jump kernel
-constexpr int MT_JUMP_PARTS = 8;
+// blocks per jump (1/parts of the coefficient words each): a whole jump on one block took ~110 us
+// of a CU; the frame-to-frame chain (each frame's key is the previous frame's end window) waited for
+// the slowest block of the jump kernel.  A part loads only the slice of y its coefficient words
+// read, so its LDS (and HBM read) shrinks with the part.
+constexpr int MT_MAX_PARTS = 8;
+constexpr int MT_MIN_PARTS = 2;
 constexpr int MT_WAVES = MT_THREADS / 64;
 constexpr int MT_G = 11;  // window outputs per lane in the jump (odd: conflict-free LDS reads; 57 lanes cover 624)
 constexpr int MT_YBLOCKS = 34;                        // 21216 words >= 32 * 623 + 10 * 63 + 42
 constexpr int MT_RED = 704;                           // per-wave stride of the reduction buffer (64 x 11)
-static_assert(rtmt::N / MT_JUMP_PARTS / MT_WAVES + 1 <= 64, "a wave's coefficient words fit one per lane");
+static_assert(rtmt::N / MT_MIN_PARTS / MT_WAVES + 1 <= 64, "a wave's coefficient words fit one per lane");
 static_assert(32 * (rtmt::N - 1) + MT_G * 63 + 32 + MT_G <= MT_YBLOCKS * rtmt::N, "jump window reads stay in y");
-static_assert(MT_WAVES * MT_RED + 3 * rtmt::N <= MT_YBLOCKS * rtmt::N, "the reduction and end ring alias y");
-constexpr size_t MT_LDS_BYTES = (size_t)MT_YBLOCKS * rtmt::N * 4;  // y
+// y words a part of coefficient words [cw0, cw0 + n) reads: y[32 cw0 ..), 32 n + the lanes' reach,
+// rounded up to whole uint4
+__host__ __device__ constexpr int mt_yslice_words(int n) { return (32 * n + MT_G * 63 + 32 + MT_G + 3) & ~3; }
+constexpr int MT_RED_WORDS = MT_WAVES * MT_RED + 3 * rtmt::N;  // the reduction, then the end ring
+__host__ __device__ constexpr int mt_jump_lds_words(int parts) {
+    return mt_yslice_words(rtmt::N / parts + 1) > MT_RED_WORDS ? mt_yslice_words(rtmt::N / parts + 1) : MT_RED_WORDS;
+}
+constexpr size_t MT_LDS_BYTES = (size_t)mt_jump_lds_words(MT_MIN_PARTS) * 4;  // the largest launch
+inline size_t mt_jump_lds_bytes(int parts) { return (size_t)mt_jump_lds_words(parts) * 4; }
 // generator threads per segment: 5 waves (227 make the next block, 312 store the current one).
 // Measured (222 segments, ex1 1080p pinhole planes): 1 wave 1.17 ms, 4 waves 0.64, 5 waves 0.50,
 // 8 waves 0.50 -- one wave is VALU-issue bound (~3000 cycles per 624-word block)
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_y(const uint32_t* key, uint32
     }
 }
 
-// Jump units, MT_JUMP_PARTS blocks each (block b: unit b / PARTS, part b % PARTS).  Tabulated mode:
+// Jump units, A.parts blocks each (block b: unit b / parts, part b % parts).  Tabulated mode:
 // unit s - 1 makes the window of segment s >= 1 into win + 624 s.  Band mode (A.bands): unit s makes
 // segment s's window into win + 624 (s + 1) (none for a band at the call's first double: it starts
 // from the key).  The windows are XOR-accumulated by their parts with atomics into the zeroed table.
@@ -195,13 +206,14 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_y(const uint32_t* key, uint32
 // to the y of that window (A.y_next), so the next frame's jump blocks need no k_mt_y.  Block 0 also
 // copies the key window to win[0] for the generators that start from it.
 __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win) {
-    extern __shared__ uint32_t mt_lds[];  // MT_YBLOCKS * 624 words
+    extern __shared__ uint32_t mt_lds[];  // mt_jump_lds_words(A.parts)
     __shared__ int last_part;
-    uint32_t* y = mt_lds;
+    uint32_t* yl = mt_lds;                    // this part's slice of y
     uint32_t* red = mt_lds;                   // MT_WAVES x MT_RED (aliases y once it is read)
     uint32_t* ring = mt_lds + MT_WAVES * MT_RED;  // end unit: 3 blocks after the reduction
-    const int unit = (int)blockIdx.x / MT_JUMP_PARTS, part = (int)blockIdx.x % MT_JUMP_PARTS;
-    const int nunits = (int)gridDim.x / MT_JUMP_PARTS;
+    const int parts = A.parts;
+    const int unit = (int)blockIdx.x / parts, part = (int)blockIdx.x % parts;
+    const int nunits = (int)gridDim.x / parts;
     const bool end_block = A.end_poly && unit == nunits - 1;
     const bool band = A.bands != nullptr;
     const int s = band ? unit : unit + 1;
@@ -210,17 +222,19 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
         for (int m = t; m < rtmt::N; m += MT_THREADS) win[m] = A.key[m];
     if (!end_block && (band ? A.bands[4 * s] == 0 : mt_seg(A, s).idle())) return;
     const uint32_t* poly = end_block ? A.end_poly : A.tab + (int64_t)(band ? s : s - 1) * rtmt::N;
+    // this part's coefficient words [p_lo, p_lo + p_n) read y[32 p_lo ..) only: that slice to LDS
+    const int p_lo = part * rtmt::N / parts, p_n = (part + 1) * rtmt::N / parts - p_lo;
     {
-        const uint4* ys = reinterpret_cast<const uint4*>(A.y);
-        uint4* yl = reinterpret_cast<uint4*>(y);
+        const uint4* ys = reinterpret_cast<const uint4*>(A.y + 32 * p_lo);
+        uint4* yq = reinterpret_cast<uint4*>(yl);
+        const int n4 = min(mt_yslice_words(p_n), MT_YBLOCKS * rtmt::N - 32 * p_lo) / 4;
 #ifndef MT_DBG_NOLOAD  // (timing harness only)
-        for (int m = t; m < MT_YBLOCKS * rtmt::N / 4; m += MT_THREADS) yl[m] = ys[m];
+        for (int m = t; m < n4; m += MT_THREADS) yq[m] = ys[m];
 #endif
     }
     __syncthreads();
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6), g = t & 63;
-    // this wave's coefficient words: part `part` of the 624, split over the waves
-    const int p_lo = part * rtmt::N / MT_JUMP_PARTS, p_n = (part + 1) * rtmt::N / MT_JUMP_PARTS - p_lo;
+    // this wave's coefficient words: its share of the part's
     const int cw_lo = p_lo + wv * p_n / MT_WAVES, cw_n = p_lo + (wv + 1) * p_n / MT_WAVES - cw_lo;
     uint32_t acc[MT_G];
 #pragma unroll
@@ -234,7 +248,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
         const uint32_t cw = __builtin_amdgcn_readlane(my_cw, ci);
         if (cw == 0u) continue;
         // y[32 cw_i + 11 g + i]: single-word loads, the odd lane stride keeps them free of bank conflicts
-        const uint32_t* yp = y + 32 * cw_i + MT_G * g;
+        const uint32_t* yp = yl + 32 * (cw_i - p_lo) + MT_G * g;
         uint32_t r[32 + MT_G];
 #pragma unroll
         for (int k = 0; k < 32 + MT_G; ++k) r[k] = yp[k];
@@ -276,7 +290,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     // window (and its y) is written, and leaves the accumulator and the counter zero
     __threadfence();
     __syncthreads();
-    if (t == 0) last_part = atomicAdd(A.end_cnt, 1u) == (uint32_t)(MT_JUMP_PARTS - 1);
+    if (t == 0) last_part = atomicAdd(A.end_cnt, 1u) == (uint32_t)(parts - 1);
     __syncthreads();
     if (!last_part) return;
     __threadfence();

@@ -100,6 +100,25 @@ def test_mt_device_1080p_jitter_stream():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 4, 8])
+def test_mt_device_jump_parts_give_the_same_stream(parts):
+    """Each jump window is XOR-accumulated by `parts` blocks over slices of the coefficient words
+    (option mt_jump_parts): every split gives numpy's stream and final state."""
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    N.check(lib, lib.srt_set_option(ctx, b"mt_jump_parts", parts))
+    try:
+        st, want, end = numpy_case(11, 17, 3_000_001, 7)
+        got, after = _device_uniforms(st, 3_000_001, 7)
+        assert np.array_equal(got, want)
+        assert after[2] == end[2] and np.array_equal(after[1], end[1])
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_jump_parts", 0))
+    assert lib.srt_set_option(ctx, b"mt_jump_parts", 1) != 0
+
+
+@pytest.mark.gpu
 def test_scene_render_device_stream_equals_host_stream():
     import scenes
 

@@ -1,6 +1,6 @@
 // Timing harness for the numpy-stream jump kernels (python-raytracer_amd/csrc/rt_mt_kernel.h):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -x hip tools/mt_jump_bench.cpp -I python-raytracer_amd/csrc \
-//         -o tools/_build/mt_jump_bench && tools/_build/mt_jump_bench [bands]
+//         -o tools/_build/mt_jump_bench && tools/_build/mt_jump_bench [bands] [parts]
 // Times (HIP events, median of 20): k_mt_y; k_mt_jump over `bands` band segments without and with the
 // end block; the end block alone; k_mt_gen over the bands.  Checks one jumped window against the
 // serial scheme (rt_mt.h jump_serial).
@@ -97,26 +97,28 @@ int main(int argc, char** argv) {
     A.dump_dst = ddump;
     A.end_acc = dacc;
     A.end_cnt = dacc + rtmt::N;
-    const int P = MT_JUMP_PARTS;
+    const int P = argc > 2 ? atoi(argv[2]) : MT_MAX_PARTS;
+    A.parts = P;
+    const size_t LDS = mt_jump_lds_bytes(P);
     float t_y = time_ms([&] { hipLaunchKernelGGL(k_mt_y, dim3(1), dim3(MT_THREADS), 0, 0, (const uint32_t*)dkey, dy); });
-    float t_j = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), MT_LDS_BYTES, 0, A, dwin); });
+    float t_j = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), LDS, 0, A, dwin); });
     MtArgs E = A;
     E.end_poly = dend;
     E.y_next = dyn;
-    float t_je = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3((nb + 1) * P), dim3(MT_THREADS), MT_LDS_BYTES, 0, E, dwin); });
+    float t_je = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3((nb + 1) * P), dim3(MT_THREADS), LDS, 0, E, dwin); });
     MtArgs E1 = E;
     E1.bands = nullptr;  // one unit: only the end window (no band segments)
-    float t_e = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(MT_THREADS), MT_LDS_BYTES, 0, E1, dwin); });
+    float t_e = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(MT_THREADS), LDS, 0, E1, dwin); });
     MtArgs E2 = E1;
     E2.y_next = nullptr;
-    float t_e2 = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(MT_THREADS), MT_LDS_BYTES, 0, E2, dwin); });
+    float t_e2 = time_ms([&] { hipLaunchKernelGGL(k_mt_jump, dim3(P), dim3(MT_THREADS), LDS, 0, E2, dwin); });
     MtArgs G = A;
     G.dump_dst = nullptr;
     float t_g = time_ms(
         [&] { hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(nb), dim3(MT_GEN_THREADS), 0, 0, G, (const uint32_t*)dwin); });
     // check band 0's window against the serial jump (windows are XOR-accumulated: zero them first)
     CK(hipMemset(dwin + rtmt::N, 0, (size_t)nb * rtmt::N * 4));
-    hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), MT_LDS_BYTES, 0, A, dwin);
+    hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), LDS, 0, A, dwin);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> w(rtmt::N), ref(rtmt::N);
     CK(hipMemcpy(w.data(), dwin + rtmt::N, rtmt::N * 4, hipMemcpyDeviceToHost));
