@@ -83,7 +83,7 @@ constexpr uint32_t ERR_NAME = 4u;         // a PointLight met by a Glossy hit (N
 // paths and scene features (the host picks the first variant covering the scene).
 constexpr uint32_t MAT_ALL = 0x3Fu;   // every material type (1 << SRT_GLOSSY .. 1 << SRT_SKY)
 constexpr uint32_t MAT_BVH = 0x40u;   // a triangle BVH (the traversal code)
-constexpr uint32_t MAT_TRI = 0x80u;   // Triangle colliders intersected one by one (collider loops)
+constexpr uint32_t MAT_TRI = 0x80u;   // Triangle colliders intersected one by one (collider loops, tie re-tests)
 constexpr uint32_t MAT_NMAP = 0x100u; // a normal-mapped material (shading_normal's texel path)
 constexpr uint32_t MAT_GENERIC = MAT_ALL | MAT_TRI | MAT_NMAP;
 constexpr uint32_t mat_bit(int type) { return 1u << type; }
@@ -710,11 +710,10 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
     const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
     uint64_t stack[BVH_STACK];
     int sp = 0;
-    stack[sp++] = bvh_entry(-INFINITY, 0);
-    while (sp > 0) {
-        const uint64_t e = stack[--sp];
-        if ((double)bvh_u2f((uint32_t)(e >> 32)) > best) continue;
-        const int32_t code = (int32_t)(uint32_t)e;
+    // the node (or leaf) visited next stays in a register: a node's nearest hit child is taken
+    // directly, the others pushed; the stack is read only when a subtree is done
+    int32_t code = 0;
+    for (;;) {
         if (code < 0) {
             const int first = (-code - 1) >> 6, cnt = (-code - 1) & 63;
             for (int j = first; j < first + cnt; ++j) {
@@ -727,14 +726,28 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
                     if (c < id) { id = c; bo = o; }
                 }
             }
-            continue;
+        } else {
+            double t[4];
+            int32_t c[4];
+            bvh_children(S.bvh[code], O, inv, best, false, t, c);
+            if (t[0] != INFINITY) {
+                RT_UNROLL
+                for (int k = 3; k >= 1; --k)
+                    if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = bvh_entry(t[k], c[k]);
+                code = c[0];
+                continue;
+            }
         }
-        double t[4];
-        int32_t c[4];
-        bvh_children(S.bvh[code], O, inv, best, false, t, c);
-RT_UNROLL
-        for (int k = 3; k >= 0; --k)
-            if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = bvh_entry(t[k], c[k]);
+        // pop the nearest pending subtree not entered beyond `best`
+        bool more = false;
+        while (sp > 0) {
+            const uint64_t e = stack[--sp];
+            if ((double)bvh_u2f((uint32_t)(e >> 32)) > best) continue;
+            code = (int32_t)(uint32_t)e;
+            more = true;
+            break;
+        }
+        if (!more) break;
     }
 }
 
@@ -743,9 +756,8 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
     const d3 inv = d3{1.0 / L.x, 1.0 / L.y, 1.0 / L.z};
     int32_t stack[BVH_STACK];
     int sp = 0;
-    stack[sp++] = 0;
-    while (sp > 0) {
-        const int32_t code = stack[--sp];
+    int32_t code = 0;
+    for (;;) {
         if (code < 0) {
             const int first = (-code - 1) >> 6, cnt = (-code - 1) & 63;
             for (int j = first; j < first + cnt; ++j) {
@@ -755,14 +767,20 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
                 const double t = triangle_hit(cc.p, O, L, o);
                 if (t < stop) return t;
             }
-            continue;
+        } else {
+            double t[4];
+            int32_t c[4];
+            bvh_children(S.bvh[code], O, inv, stop, true, t, c);
+            if (t[0] != INFINITY) {
+                RT_UNROLL
+                for (int k = 3; k >= 1; --k)
+                    if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = c[k];
+                code = c[0];
+                continue;
+            }
         }
-        double t[4];
-        int32_t c[4];
-        bvh_children(S.bvh[code], O, inv, stop, true, t, c);
-RT_UNROLL
-        for (int k = 3; k >= 0; --k)
-            if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = c[k];
+        if (sp == 0) break;
+        code = stack[--sp];
     }
     return FARAWAY;
 }

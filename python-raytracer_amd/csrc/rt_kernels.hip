@@ -1201,9 +1201,9 @@ const Variant VARIANTS[] = {
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
     {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
     // a glossy TriangleMesh in the ex1 setting (the mesh bench): the BVH traversal, no other features
-    {MATS_GLOSSY_SKY | MAT_BVH, k_primary<MATS_GLOSSY_SKY | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_BVH, OCC>,
-     k_frame<MATS_GLOSSY_SKY | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_BVH, OCC, true>,
-     k_primary<MATS_GLOSSY_SKY | MAT_BVH, RT_FUSE_OCC, true>},
+    {MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>,
+     k_frame<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC, true>,
+     k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, RT_FUSE_OCC, true>},
     {MAT_GENERIC, k_primary<MAT_GENERIC, OCC>, k_trace<MAT_GENERIC, OCC>, k_frame<MAT_GENERIC, OCC>,
      k_trace<MAT_GENERIC, OCC, true>},
     // scenes with a triangle BVH (TriangleMesh)
@@ -2668,7 +2668,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     c->fanout = fan;
     c->mats = 0;
     for (int i = 0; i < d->n_materials; ++i) c->mats |= mat_bit(d->materials[i].type);
-    if (S.bvh_nodes > 0) c->mats |= MAT_BVH;
+    if (S.bvh_nodes > 0) c->mats |= MAT_BVH | MAT_TRI;  // (a tied ray re-tests its colliders, triangles too)
     if (lin_tri) c->mats |= MAT_TRI;  // Triangle colliders outside the BVH
     for (int i = 0; i < d->n_materials; ++i)
         if (d->materials[i].normalmap >= 0) c->mats |= MAT_NMAP;

@@ -243,22 +243,29 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     // adds y[32 cw_i + j + 11 g + k] to the lane's eleven outputs k.  The wave's coefficient words
     // are held one per lane and read out by v_readlane.
     const uint32_t my_cw = g < cw_n ? poly[cw_lo + g] : 0u;
+    // the lane's window slides by 32 words from one coefficient word to the next: its last 11 words
+    // are the next window's first (loaded once); a zero word still slides the window
+    uint32_t r[32 + MT_G];
+    {
+        const uint32_t* yp = yl + 32 * (cw_lo - p_lo) + MT_G * g;
+#pragma unroll
+        for (int k = 0; k < MT_G; ++k) r[32 + k] = yp[k];
+    }
     for (int ci = 0; ci < cw_n; ++ci) {
         const int cw_i = cw_lo + ci;
         const uint32_t cw = __builtin_amdgcn_readlane(my_cw, ci);
-        if (cw == 0u) continue;
         // y[32 cw_i + 11 g + i]: single-word loads, the odd lane stride keeps them free of bank conflicts
         const uint32_t* yp = yl + 32 * (cw_i - p_lo) + MT_G * g;
-        uint32_t r[32 + MT_G];
 #pragma unroll
-        for (int k = 0; k < 32 + MT_G; ++k) r[k] = yp[k];
-        // bit pairs: pattern 01 / 10 adds one shifted row, 11 the pre-XORed pair row d (one XOR per
+        for (int k = 0; k < MT_G; ++k) r[k] = r[32 + k];
+#pragma unroll
+        for (int k = MT_G; k < 32 + MT_G; ++k) r[k] = yp[k];
+        if (cw == 0u) continue;
+        // bit pairs: pattern 01 / 10 adds one shifted row, 11 both rows (one three-input XOR per
         // output either way; a uniform branch per pair).  Measured per jump block (tools/
-        // mt_jump_bench.cpp, 204 bands): pairs 74 us; a v_bitop3 acc ^= y & mask per bit, branch-free,
-        // 117 us; a uniform branch per bit 108 us; nibbles (xor3 of two pair rows) 172 us
-        uint32_t d[32 + MT_G - 1];
-#pragma unroll
-        for (int k = 0; k < 32 + MT_G - 1; ++k) d[k] = r[k] ^ r[k + 1];
+        // mt_jump_bench.cpp, 204 bands): pairs with a pre-XORed pair row 74 us; a v_bitop3 acc ^= y &
+        // mask per bit, branch-free, 117 us; a uniform branch per bit 108 us; nibbles (xor3 of two pair
+        // rows) 172 us
 #pragma unroll
         for (int j = 0; j < 32; j += 2) {
             const uint32_t pat = (cw >> j) & 3u;  // wave-uniform
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
                 for (int k = 0; k < MT_G; ++k) acc[k] ^= r[j + 1 + k];
             } else if (pat == 3u) {
 #pragma unroll
-                for (int k = 0; k < MT_G; ++k) acc[k] ^= d[j + k];
+                for (int k = 0; k < MT_G; ++k) acc[k] = __builtin_amdgcn_bitop3_b32(acc[k], r[j + k], r[j + 1 + k], 0x96);
             }
         }
     }

@@ -482,10 +482,11 @@ def test_gpu_async_numpy_stream_frames_match_sync_frames():
         assert np.array_equal(rgb, ref[k].rgb)
 
 
-@pytest.mark.parametrize("mode", ["wavefront", "frame"])
+@pytest.mark.parametrize("mode", ["wavefront", "frame", "fused"])
 def test_gpu_triangle_mesh_bvh_matches_oracle(tmp_path, mode):
     """TriangleMesh through the device BVH (320 triangles + a tie-making duplicate set) against the
-    oracle's linear loop over the collider list: hit ids exact, per-depth counts, RGB."""
+    oracle's linear loop over the collider list: hit ids exact, per-depth counts, RGB -- per-depth
+    kernels, the frame kernel, and the fused single-child paths (the glossy BVH variant)."""
     for dup in (0, 12):
         path = str(tmp_path / ("ico%d.obj" % dup))
         scenes.write_icosphere_obj(path, subdiv=2, duplicate_faces=dup)
@@ -493,10 +494,12 @@ def test_gpu_triangle_mesh_bvh_matches_oracle(tmp_path, mode):
         np.random.seed(9)
         jit = sc.camera.draw_jitter(2)
         _set_option("frame_kernel", 1 if mode == "frame" else 0)
+        _set_option("fuse_primary", 1 if mode == "fused" else 0)
         try:
             out = _backend().render_scene(sc, 2, jitter=jit, seed=1, want_hits=True)
         finally:
             _set_option("frame_kernel", -1)
+            _set_option("fuse_primary", -1)
         rgb, ids, counts = O.render_linear(sc, jit)
         assert np.array_equal(out.hit_ids, ids)
         assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
