@@ -28,9 +28,6 @@ structured like the reference's Scene.render).
 import os
 
 os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")  # CPU baseline legs: one BLAS thread per process
-# seven hardware queues per process (HIP's default is four; read when HIP initialises, inherited by the
-# ranks): the library then keeps six frames in flight (rt_kernels.hip default_slots)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "7")
 import argparse
 import ctypes
 import json
@@ -492,6 +489,11 @@ def main():
     ap.add_argument("--size", default=None, help="diagnostic: WxH override of the config's frame size")
     ap.add_argument("--option", action="append", default=[],
                     help="experiment: srt_set_option KEY=VALUE before rendering (repeatable)")
+    ap.add_argument("--hw-queues", type=int, default=7,
+                    help="GPU_MAX_HW_QUEUES for this process (read when HIP initialises): the library keeps one "
+                         "frame in flight per hardware queue but one (rt_kernels.hip default_slots); 7 -> six "
+                         "frames.  Set here, not inherited: the GPU boxes export HIP's default of 4, which "
+                         "leaves four frame slots sharing three queues")
     ap.add_argument("--device-outputs", action="store_true",
                     help="diagnostic (one process): the frames' outputs left in HBM instead of host memory")
     ap.add_argument("--sync", action="store_true",
@@ -508,6 +510,9 @@ def main():
     ap.add_argument("--shard-snake", type=int, default=-1,
                     help="band dealing order, 0 round-robin / 1 snake (library option shard_snake; default SHARD_SNAKE)")
     args = ap.parse_args()
+    if not 1 <= args.hw_queues <= 32:
+        raise SystemExit("bench.py: --hw-queues 1 .. 32")
+    os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)  # (before anything initialises HIP)
 
     plan = launch_plan(args.gpus, os.environ, visible_gpus() if "WORLD_SIZE" not in os.environ and args.gpus > 1
                        else args.gpus, sys.argv[1:])
@@ -630,7 +635,7 @@ def main():
         # does not carry the GPU's own warm-up into the slowest-rank figure
         prime_s = 0.5 if (i == 0 and len(rehearse) > 1) else 0.0
         while w < args.warmup or time.perf_counter() - t_w < prime_s:
-            step(async_ok=w > 0)  # the first frame runs synchronously (sizes queues and rings)
+            step(async_ok=w > 0 and not args.sync)  # the first frame runs synchronously (sizes queues and rings)
             w += 1
             if w % 50 == 0:
                 barrier()  # (bounded queue depth while priming)

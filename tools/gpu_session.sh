@@ -40,7 +40,7 @@ for step in "$@"; do
           done ;;
     shardall) for C in ${SHARD_CONFIGS:-example1_1080p_d5 example4_4k_d6 cornell_800_s512}; do
                 case $C in cornell*) st=2;; example4*) st=10;; *) st=100;; esac
-                run "whole_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup 2
+                run "whole_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup $((st > 50 ? 300 : 2))
                 for n in ${SHARD_NS:-2 4 8}; do
                   run "shard${n}_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup 2 --shard-of $n --shard-rank all
                 done
