@@ -64,7 +64,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 848;
+constexpr size_t TRACE_PARAMS_BYTES = 856;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
@@ -1831,6 +1831,13 @@ int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
 }
 
 size_t lut_bytes(const srt_ctx* c) { return (size_t)c->S.nlut_lds * 256 * sizeof(double); }
+// RT_BVH_LDS builds: the BLOCK-thread trace kernels of a BVH scene keep their traversal stacks' first
+// entries in LDS after the tables (SceneView::bvh_lds)
+#ifdef RT_BVH_LDS
+size_t bvh_lds_bytes(const srt_ctx* c) { return (c->mats & MAT_BVH) ? (size_t)BVH_LDS_ENTRIES * 8 * BLOCK : 0; }
+#else
+size_t bvh_lds_bytes(const srt_ctx*) { return 0; }
+#endif
 
 int trace_grid(const srt_ctx* c) { return std::max(NSHARD, (c->max_blocks / NSHARD) * NSHARD); }
 
@@ -3096,9 +3103,11 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.out_u8 = res_u8;
             P.spp_total = a->spp;
             if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
+            P.S.bvh_lds = bvh_lds_bytes(c) > 0 && PIX_LDS_BYTES + COLD_LDS_BYTES == 0;
             hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
-                               lut_bytes(c) + PIX_LDS_BYTES + COLD_LDS_BYTES, c->f->stream, P);
+                               lut_bytes(c) + PIX_LDS_BYTES + COLD_LDS_BYTES + (P.S.bvh_lds ? bvh_lds_bytes(c) : 0),
+                               c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
@@ -3117,8 +3126,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 P.cnt_out = c->f->counts + (int64_t)(d + 1) * NSHARD;
                 P.chain = (d == F.chain_from);
                 P.dcap = F.dcap;
-                hipLaunchKernelGGL(P.chain ? V.chain : V.trace, dim3(trace_grid(c)), dim3(BLOCK), lut_bytes(c), c->f->stream,
-                                   P);
+                hipLaunchKernelGGL(P.chain ? V.chain : V.trace, dim3(trace_grid(c)), dim3(BLOCK),
+                                   lut_bytes(c) + bvh_lds_bytes(c), c->f->stream, P);
                 HIP_TRY(hipGetLastError());
                 HIP_TRY(hipEventRecord(ev[1 + d], c->f->stream));
             }
