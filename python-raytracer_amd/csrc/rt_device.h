@@ -247,13 +247,9 @@ struct SceneView {
     const RT_RO int32_t* bvh_tri;  // collider index of each BVH leaf slot
     int bvh_nodes;                 // 0: no BVH
     int sky_col;                   // the one collider shaded by a SkyBox / Panorama material, else -1
-    // the kernel's dynamic LDS holds, after the texture tables, BVH_LDS_ENTRIES traversal stack
-    // entries per thread (builds with RT_BVH_LDS; set by the host for the launches that reserve them)
-    int bvh_lds;
-    int pad_;
 };
 // the host builds SceneView/TraceParams and the device reads them: the layout must agree
-static_assert(sizeof(SceneView) == 184 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
+static_assert(sizeof(SceneView) == 176 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
 
 // BVH node, 4-wide (128 B: one traversal step loads one cache line and tests four boxes): child k's
 // box [lo[.][k], hi[.][k]] in float, rounded outward from the build's f64 boxes (which are inflated so
@@ -268,7 +264,6 @@ struct BvhNode {
 static_assert(sizeof(BvhNode) == 128, "one 128-byte line per BVH node");
 constexpr int32_t BVH_EMPTY = (int32_t)0x80000000;
 constexpr int BVH_STACK = 32;  // (3 entries per 4-wide level at most: depth <= 10 levels)
-constexpr int BVH_LDS_ENTRIES = 16;  // RT_BVH_LDS: the stack's first entries in LDS (8 B each per thread)
 
 // The kernel's dynamic LDS: the texture tables [0, nlut_lds) staged by the trace kernels first
 // (rt_kernels.hip stage_luts), read directly (no pointer in the scene view, so the kernels' scene view
@@ -673,30 +668,6 @@ RT_HD uint64_t bvh_entry(double tn, int32_t code) {
     if ((double)f > tn) f = nextafterf(f, -INFINITY);
     return ((uint64_t)bvh_f2u(f) << 32) | (uint32_t)code;
 }
-// The traversal stack: a private array, or (RT_BVH_LDS, S.bvh_lds) its first BVH_LDS_ENTRIES entries
-// in the kernel's dynamic LDS after the texture tables, one 8-byte slot per thread and entry
-// (lane-interleaved: a wave's accesses are consecutive)
-struct BvhStack {
-    uint64_t priv[BVH_STACK];
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RT_BVH_LDS)
-    RT_LDS uint64_t* lds;
-    int stride;
-    __device__ explicit BvhStack(const SceneView& S) {
-        lds = S.bvh_lds ? (RT_LDS uint64_t*)(rt_lds_dyn + S.nlut_lds * 256) + threadIdx.x : nullptr;
-        stride = (int)blockDim.x;
-    }
-    __device__ void put(int i, uint64_t e) {
-        if (lds && i < BVH_LDS_ENTRIES) lds[i * stride] = e;
-        else priv[i] = e;
-    }
-    __device__ uint64_t get(int i) const { return (lds && i < BVH_LDS_ENTRIES) ? lds[i * stride] : priv[i]; }
-#else
-    RT_HDM explicit BvhStack(const SceneView&) {}
-    RT_HDM void put(int i, uint64_t e) { priv[i] = e; }
-    RT_HDM uint64_t get(int i) const { return priv[i]; }
-#endif
-};
-
 RT_HD int32_t bvh_code(int32_t child, int32_t count) {
     return child >= 0 ? child : -(1 + (((-child - 1) << 6) | count));
 }
@@ -737,7 +708,7 @@ RT_UNROLL
 // misses).
 RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
     const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
-    BvhStack stack(S);
+    uint64_t stack[BVH_STACK];
     int sp = 0;
     // the node (or leaf) visited next stays in a register: a node's nearest hit child is taken
     // directly, the others pushed; the stack is read only when a subtree is done
@@ -762,7 +733,7 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
             if (t[0] != INFINITY) {
                 RT_UNROLL
                 for (int k = 3; k >= 1; --k)
-                    if (t[k] != INFINITY && sp < BVH_STACK) stack.put(sp++, bvh_entry(t[k], c[k]));
+                    if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = bvh_entry(t[k], c[k]);
                 code = c[0];
                 continue;
             }
@@ -770,7 +741,7 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
         // pop the nearest pending subtree not entered beyond `best`
         bool more = false;
         while (sp > 0) {
-            const uint64_t e = stack.get(--sp);
+            const uint64_t e = stack[--sp];
             if ((double)bvh_u2f((uint32_t)(e >> 32)) > best) continue;
             code = (int32_t)(uint32_t)e;
             more = true;
@@ -783,7 +754,7 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
 // Any shadowed BVH triangle closer than `stop` along L: returns its distance, else FARAWAY.
 RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
     const d3 inv = d3{1.0 / L.x, 1.0 / L.y, 1.0 / L.z};
-    BvhStack stack(S);
+    int32_t stack[BVH_STACK];
     int sp = 0;
     int32_t code = 0;
     for (;;) {
@@ -803,13 +774,13 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
             if (t[0] != INFINITY) {
                 RT_UNROLL
                 for (int k = 3; k >= 1; --k)
-                    if (t[k] != INFINITY && sp < BVH_STACK) stack.put(sp++, (uint32_t)c[k]);
+                    if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = c[k];
                 code = c[0];
                 continue;
             }
         }
         if (sp == 0) break;
-        code = (int32_t)(uint32_t)stack.get(--sp);
+        code = stack[--sp];
     }
     return FARAWAY;
 }

@@ -64,7 +64,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 856;
+constexpr size_t TRACE_PARAMS_BYTES = 848;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
@@ -1752,6 +1752,16 @@ int ensure_buf(T** p, int64_t& cap, int64_t count) {
     return SRT_OK;
 }
 
+// The segment-window table of a slot's numpy-stream generation: zero when (re)allocated; from then
+// on every window a jump XORs into is zeroed again by the generator that reads it
+int mt_win_ensure(uint32_t** p, int64_t& cap, int64_t count) {
+    if (count <= cap && *p) return SRT_OK;
+    int rc = ensure_buf(p, cap, count);
+    if (rc) return rc;
+    HIP_TRY(hipMemset(*p, 0, (size_t)count * 4));
+    return SRT_OK;
+}
+
 template <typename T>
 int upload(srt_ctx* c, const T* src, int64_t count, T** dst) {
     *dst = nullptr;
@@ -1831,13 +1841,6 @@ int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
 }
 
 size_t lut_bytes(const srt_ctx* c) { return (size_t)c->S.nlut_lds * 256 * sizeof(double); }
-// RT_BVH_LDS builds: the BLOCK-thread trace kernels of a BVH scene keep their traversal stacks' first
-// entries in LDS after the tables (SceneView::bvh_lds)
-#ifdef RT_BVH_LDS
-size_t bvh_lds_bytes(const srt_ctx* c) { return (c->mats & MAT_BVH) ? (size_t)BVH_LDS_ENTRIES * 8 * BLOCK : 0; }
-#else
-size_t bvh_lds_bytes(const srt_ctx*) { return 0; }
-#endif
 
 int trace_grid(const srt_ctx* c) { return std::max(NSHARD, (c->max_blocks / NSHARD) * NSHARD); }
 
@@ -2055,8 +2058,8 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     A.end_acc = mt_end_acc(c);
     A.end_cnt = mt_end_cnt(c);
     A.parts = mt_jump_parts(c);
-    // the segment windows are XOR-accumulated by their jump parts
-    HIP_TRY(hipMemsetAsync(win + rtmt::N, 0, (size_t)T.nseg * rtmt::N * 4, st));
+    // the segment windows are XOR-accumulated by their jump parts into the table, which is zero here:
+    // zeroed when allocated (mt_win_ensure), and every generator zeroes the window it read
     hipLaunchKernelGGL(k_mt_jump, dim3((T.nseg + 1) * A.parts), dim3(MT_THREADS), mt_jump_lds_bytes(A.parts), st, A,
                        win);
     HIP_TRY(hipGetLastError());
@@ -2064,7 +2067,7 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     MtArgs G = A;
     G.dump_dst = nullptr;
     G.y_next = nullptr;
-    hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, st, G, (const uint32_t*)win);
+    hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
     HIP_TRY(hipGetLastError());
     c->mt_y_valid[c->mt_cur ^ 1] = true;
     c->mt_cur ^= 1;
@@ -2119,8 +2122,8 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
             A.end_acc = mt_end_acc(c);
             A.end_cnt = mt_end_cnt(c);
             A.parts = mt_jump_parts(c);
-            // the segment windows are XOR-accumulated by their jump parts
-            if (R.nseg > 1) HIP_TRY(hipMemsetAsync(win + rtmt::N, 0, (size_t)(R.nseg - 1) * rtmt::N * 4, st));
+            // the segment windows are XOR-accumulated by their jump parts (into zeroed windows: see
+            // mt_launch_bands)
             hipLaunchKernelGGL(k_mt_jump, dim3(jump_blocks * A.parts), dim3(MT_THREADS), mt_jump_lds_bytes(A.parts),
                                st, A, win);
             HIP_TRY(hipGetLastError());
@@ -2129,7 +2132,7 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
         MtArgs G = A;
         G.y_next = nullptr;
         if (end) G.dump_dst = nullptr;  // (made by the jump kernel)
-        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, G, (const uint32_t*)win);
+        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
         HIP_TRY(hipGetLastError());
     }
     c->mt_cur ^= 1;
@@ -2882,7 +2885,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
-        if (!r && use_mt) r = ensure_buf(&c->f->mt_win, c->f->mt_win_cap, mt_win_need);
+        if (!r && use_mt) r = mt_win_ensure(&c->f->mt_win, c->f->mt_win_cap, mt_win_need);
         if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
         if (!r && sharded && c->rank == 0) {
             r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, c->nranks * maxpix * 3);
@@ -3103,11 +3106,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             P.out_u8 = res_u8;
             P.spp_total = a->spp;
             if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
-            P.S.bvh_lds = bvh_lds_bytes(c) > 0 && PIX_LDS_BYTES + COLD_LDS_BYTES == 0;
             hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
-                               lut_bytes(c) + PIX_LDS_BYTES + COLD_LDS_BYTES + (P.S.bvh_lds ? bvh_lds_bytes(c) : 0),
-                               c->f->stream, P);
+                               lut_bytes(c) + PIX_LDS_BYTES + COLD_LDS_BYTES, c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
@@ -3127,7 +3128,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 P.chain = (d == F.chain_from);
                 P.dcap = F.dcap;
                 hipLaunchKernelGGL(P.chain ? V.chain : V.trace, dim3(trace_grid(c)), dim3(BLOCK),
-                                   lut_bytes(c) + bvh_lds_bytes(c), c->f->stream, P);
+                                   lut_bytes(c), c->f->stream, P);
                 HIP_TRY(hipGetLastError());
                 HIP_TRY(hipEventRecord(ev[1 + d], c->f->stream));
             }
@@ -3683,7 +3684,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     hipStream_t st = c->f->stream;
     HIP_TRY(hipMemcpyAsync(mt_key0(c), key, rtmt::N * 4, hipMemcpyHostToDevice, st));
     int final_pos = 0;
-    if ((rc = ensure_buf(&c->f->mt_win, c->f->mt_win_cap, (int64_t)rtmt::SEGS * rtmt::N))) return rc;
+    if ((rc = mt_win_ensure(&c->f->mt_win, c->f->mt_win_cap, (int64_t)rtmt::SEGS * rtmt::N))) return rc;
     if ((rc = mt_launch(c, st, c->f->mt_win, mt_key0(c), pos, n_out, n_skip, dst, &final_pos))) return rc;
     if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(key_out, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost, st));

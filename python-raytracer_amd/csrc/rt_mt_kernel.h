@@ -1,6 +1,7 @@
 // rt_mt_kernel.h -- the device generator of numpy's legacy `np.random.rand` stream (rt_mt.h):
-// k_mt_round, one workgroup per 2^19-word segment of a round.  Included by rt_kernels.hip (the
-// library) and tools/mt_bench.hip (a stand-alone timing harness for this kernel).
+// k_mt_y, k_mt_jump (segment start windows by jump polynomials) and k_mt_gen (the segments' words,
+// tempered to doubles).  Included by rt_kernels.hip (the library) and tools/mt_jump_bench.cpp (a
+// stand-alone timing harness).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -322,17 +323,27 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
 
 // NT threads per segment: generate from its window (the key for segment 0) and store its doubles.
 // NT = 64: one wave (no workgroup barrier, the next block in three staged chunks); NT >= 256: the
-// workgroup form (threads < 227 make three words each)
+// workgroup form (threads < 227 make three words each).  The window, once read, is zeroed for the
+// next generation's jump parts to XOR into (no memset launch on the generation's critical path:
+// behind the trace kernels of the frames in flight a 150 KB fill waited 36-133 us for a CU).
 template <int NT>
-__global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, const uint32_t* win) {
+__global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, uint32_t* win) {
     __shared__ uint32_t ring[3 * rtmt::N];
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const MtSeg g = mt_seg(A, s);
-    if (g.idle()) return;
-    const uint32_t* w0p = A.bands ? (g.ws == 0 ? win : win + (int64_t)(s + 1) * rtmt::N)
-                                  : (s == 0 && !A.key_in_win) ? A.key : win + (int64_t)s * rtmt::N;
-    for (int m = lane; m < rtmt::N; m += NT) ring[m] = w0p[m];
+    uint32_t* w0p = A.bands ? (g.ws == 0 ? win : win + (int64_t)(s + 1) * rtmt::N)
+                            : (s == 0 && !A.key_in_win) ? nullptr : win + (int64_t)s * rtmt::N;
+    if (g.idle()) {
+        if (w0p)
+            for (int m = lane; m < rtmt::N; m += NT) w0p[m] = 0u;
+        return;
+    }
+    const uint32_t* src = w0p ? w0p : A.key;
+    for (int m = lane; m < rtmt::N; m += NT) {
+        ring[m] = src[m];
+        if (w0p) w0p[m] = 0u;  // (each thread zeroes the words it read)
+    }
     __syncthreads();
     // block q holds words ws + 624 q .. + 623 and stores the pairs whose second word it holds
     const int off0 = (int)(g.lo - g.ws);  // 1 .. 625 (s > 0) or pos (s == 0)

@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
     MtArgs G = A;
     G.dump_dst = nullptr;
     float t_g = time_ms(
-        [&] { hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(nb), dim3(MT_GEN_THREADS), 0, 0, G, (const uint32_t*)dwin); });
+        [&] { hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(nb), dim3(MT_GEN_THREADS), 0, 0, G, dwin); });
     // check band 0's window against the serial jump (windows are XOR-accumulated: zero them first)
     CK(hipMemset(dwin + rtmt::N, 0, (size_t)nb * rtmt::N * 4));
     hipLaunchKernelGGL(k_mt_jump, dim3(nb * P), dim3(MT_THREADS), LDS, 0, A, dwin);
