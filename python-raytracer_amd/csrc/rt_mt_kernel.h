@@ -201,8 +201,9 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_y(const uint32_t* key, uint32
 // unit s - 1 makes the window of segment s >= 1 into win + 624 s.  Band mode (A.bands): unit s makes
 // segment s's window into win + 624 (s + 1) (none for a band at the call's first double: it starts
 // from the key).  The windows are XOR-accumulated by their parts with atomics into the zeroed table.
-// With A.end_poly the last unit instead jumps to the window at A.end_at (into A.end_acc), and its part
-// that arrives last generates forward to the final window (A.dump_at), written to A.dump_dst -- the
+// With A.end_poly unit 0 (dispatched first: the next frame's generation waits for it, the segment
+// windows only this frame's generators) jumps to the window at A.end_at (into A.end_acc), the
+// segment units follow it, and its part that arrives last generates forward to the final window (A.dump_at), written to A.dump_dst -- the
 // next frame's key, ready when this kernel ends (its whole generation need not have run) -- and on
 // to the y of that window (A.y_next), so the next frame's jump blocks need no k_mt_y.  Block 0 also
 // copies the key window to win[0] for the generators that start from it.
@@ -213,9 +214,9 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
     uint32_t* red = mt_lds;                   // MT_WAVES x MT_RED (aliases y once it is read)
     uint32_t* ring = mt_lds + MT_WAVES * MT_RED;  // end unit: 3 blocks after the reduction
     const int parts = A.parts;
-    const int unit = (int)blockIdx.x / parts, part = (int)blockIdx.x % parts;
-    const int nunits = (int)gridDim.x / parts;
-    const bool end_block = A.end_poly && unit == nunits - 1;
+    const int part = (int)blockIdx.x % parts;
+    const bool end_block = A.end_poly && (int)blockIdx.x < parts;
+    const int unit = (int)blockIdx.x / parts - (A.end_poly ? 1 : 0);  // segment unit (end unit: -1)
     const bool band = A.bands != nullptr;
     const int s = band ? unit : unit + 1;
     const int t = threadIdx.x;
