@@ -503,8 +503,9 @@ def main():
                     help="diagnostic (1 GPU): render only one rank's rows of an N-rank job (its per-frame work "
                          "without the gather)")
     ap.add_argument("--shard-rank", default="0",
-                    help="with --shard-of: the rank rehearsed, or 'all' (every rank in turn; ms_per_step = the "
-                         "slowest rank, value = all ranks' rays / that time)")
+                    help="with --shard-of: the rank rehearsed, or 'all' / 'all-reversed' (every rank in turn, "
+                         "from rank 0 or from the last; ms_per_step = the slowest rank, value = all ranks' rays / "
+                         "that time)")
     ap.add_argument("--shard-bands", type=int, default=0,
                     help="most row bands per rank (library option shard_bands; default rt_device.h shard_kmax)")
     ap.add_argument("--shard-snake", type=int, default=-1,
@@ -573,7 +574,8 @@ def main():
     snake = args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE
     rehearse = {None: None}  # rank -> its rows (None: the frame as the launcher splits it)
     if args.shard_of > 1 and world == 1:
-        ranks = range(args.shard_of) if args.shard_rank == "all" else [int(args.shard_rank)]
+        ranks = (range(args.shard_of) if args.shard_rank == "all" else
+                 range(args.shard_of - 1, -1, -1) if args.shard_rank == "all-reversed" else [int(args.shard_rank)])
         rehearse = {r: np.ascontiguousarray(shard_rows(H, args.shard_of, r, kmax, snake), dtype=np.int32)
                     for r in ranks}
         rows32 = rehearse[min(ranks)]
@@ -631,9 +633,9 @@ def main():
             a.rows, a.n_rows = N.ptr(rows32), len(rows32)
         t_w = time.perf_counter()
         w = 0
-        # rehearsing several ranks: the first one's warm-up also runs >= 0.5 s of frames, so that it
+        # rehearsing several ranks: the first one's warm-up also runs >= 1.5 s of frames, so that it
         # does not carry the GPU's own warm-up into the slowest-rank figure
-        prime_s = 0.5 if (i == 0 and len(rehearse) > 1) else 0.0
+        prime_s = 1.5 if (i == 0 and len(rehearse) > 1) else 0.0
         while w < args.warmup or time.perf_counter() - t_w < prime_s:
             step(async_ok=w > 0 and not args.sync)  # the first frame runs synchronously (sizes queues and rings)
             w += 1
@@ -747,8 +749,10 @@ def main():
                                      "band_height": band_height(H, max(world, args.shard_of, 1), kmax, snake)}},
         }
         if len(rehearse) > 1:
-            rec["rank_frame_ms"] = [round(x, 4) for x in rank_ms]
-            rec["rank_rays"] = rank_rays
+            order = list(rehearse)  # (rank of each rehearsal, in the order run)
+            rec["rank_frame_ms"] = [round(rank_ms[order.index(r)], 4) for r in sorted(order)]
+            rec["rank_rays"] = [rank_rays[order.index(r)] for r in sorted(order)]
+            rec["rehearsal_order"] = order
         if sec:
             rec["config"]["frame_latency_ms"] = sec["frame_latency_ms"]
             if "device_resident" in sec:
