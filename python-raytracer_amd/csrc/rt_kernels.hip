@@ -1632,10 +1632,11 @@ struct srt_ctx {
     // slowest rank 0.318 -> 0.265 ms per frame, the whole ex1 frame 1.30 -> 1.26 ms (8 slots: 0.41 /
     // 1.28; profiles/r03_slots_ab.txt)
     int nslots = 4;
-    // -1 auto: a high-priority stream of its own for frames of more than a third of the rows (ex1 1080p
-    // 1.80 -> 1.64 ms/frame, same box; one rank of 2: 0.989 -> 0.926 ms), the frame's stream for
-    // smaller shards (one rank of 4: 0.581 vs 0.608, of 8: 0.340 vs 0.363); 0 the frame's stream;
-    // 1 a stream of its own (0.580 / 0.339: as 0); 2 a high-priority one
+    // -1 auto: a high-priority stream of its own for whole frames (ex1 1080p 1.80 -> 1.64 ms/frame, same
+    // box), the frame's stream for shards (round 4, same box: one rank of 2 0.87 ms on a stream of its
+    // own, 0.67 on a high-priority one, 0.55 on the frame's stream; of 4 0.33 / 0.48 / 0.32; of 8
+    // 0.20 / 0.33 / 0.21, profiles/r04_mt_stream_ab.txt); 0 the frame's stream; 1 a stream of its own;
+    // 2 a high-priority one
     int use_mt_stream = -1;
     bool use_copy_stream = false;
     // option "deterministic" (default 1): contributions added to a pixel by other threads go into
@@ -2957,14 +2958,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         // (it waits until the slot's previous frame has read its jitter), else the frame's stream
         hipStream_t mst = c->f->stream;
         if (use_mt) {
-            // (more than a third of the rows: whole frames and both ranks of a 2-rank frame, whose
-            // shards differ by a band)
-            // (auto: whole frames on the high-priority stream; a shard of more than a third of the
-            // rows -- a rank of 2 -- on a stream of its own at normal priority: 6 slots, same box,
-            // slowest of 2 ranks 0.79 / 0.79 ms vs 0.71 / 1.07 on the high-priority one and 1.08 / 1.07
-            // on the frame's stream, profiles/r03_mt_stream_ab.txt)
-            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream
-                                                  : (n_rows >= Hf ? 2 : (3 * (int64_t)n_rows > Hf ? 1 : 0));
+            // (auto: whole frames on the high-priority stream, shards on the frame's stream: a stream
+            // shared by the frames serialises their generations, and a shard's band segments -- one
+            // serial generator block each -- are long: a rank of 2's 130k-double bands take ~0.4 ms)
+            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream : (n_rows >= Hf ? 2 : 0);
             if (F.npass == 1 && mts) {
                 if (!c->mt_stream) {
                     // a high-priority queue (mt_stream 2): the generation's blocks are dispatched ahead
