@@ -1838,6 +1838,12 @@ int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
     const int64_t want = fused ? fused_items(c) : (int64_t)c->max_blocks * 64;
     int g = 1;
     while (g * 2 <= std::min(ns, 64) && npix * g < want) g *= 2;
+    // a BVH scene's paths differ widely in length (mesh hits traverse, the rest do not): one sample
+    // per lane where the spp allows (up to 4 groups, dividing the samples evenly) gives the GPU twice
+    // the waves to balance -- mesh 1080p 2 spp 5.94 -> 4.33 ms per frame, same box
+    // (profiles/r04_mesh_pix_groups_ab.txt); the uniform ex1 frame is faster with G = 1 (1.08 vs 1.14 ms)
+    if (c->mats & MAT_BVH)
+        while (g * 2 <= std::min(ns, 4) && ns % (g * 2) == 0) g *= 2;
     return g;
 }
 
