@@ -1841,9 +1841,13 @@ int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
     // a BVH scene's paths differ widely in length (mesh hits traverse, the rest do not): one sample
     // per lane where the spp allows (up to 4 groups, dividing the samples evenly) gives the GPU twice
     // the waves to balance -- mesh 1080p 2 spp 5.94 -> 4.33 ms per frame, same box
-    // (profiles/r04_mesh_pix_groups_ab.txt); the uniform ex1 frame is faster with G = 1 (1.08 vs 1.14 ms)
+    // (profiles/r04_mesh_pix_groups_ab.txt)
     if (c->mats & MAT_BVH)
         while (g * 2 <= std::min(ns, 4) && ns % (g * 2) == 0) g *= 2;
+    // the fused paths take two groups whenever the samples split evenly: ex1 1080p 6 spp, same box,
+    // the fused kernel 1.095 -> 1.050 ms per launch, device-resident frame 0.841 -> 0.830 ms
+    // (profiles/r04_pix_groups_ab.txt)
+    if (fused && g < 2 && ns % 2 == 0) g = 2;
     return g;
 }
 
