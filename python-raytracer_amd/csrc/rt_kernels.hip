@@ -308,60 +308,6 @@ struct PixAcc {
     }
 };
 
-// RT_PIX_LDS: the thread's PixAcc kept in LDS (its own slot; 28 B per thread after the texture
-// tables) instead of 7 VGPRs live across the whole trace: fixed-point terms are fire-and-forget
-// ds_add_u64 / ds_add_f32 (integer sums: exact in any order), f64 terms read-modify-write
-#ifdef RT_PIX_LDS
-struct PixAccLds {
-    RT_LDS unsigned long long* w;  // w[0], w[BLOCK], w[2 BLOCK]: this thread's three sums
-    RT_LDS float* mag;
-
-    __device__ __forceinline__ void zero() {
-        w[0] = 0ull;
-        w[BLOCK] = 0ull;
-        w[2 * BLOCK] = 0ull;
-        *mag = 0.0f;
-    }
-    __device__ __forceinline__ void add(bool fx, d3 t) {
-        if (fx) {
-            const double m = (fabs(t.x) + fabs(t.y)) + fabs(t.z);
-            if (m < FX_MAX) {
-                __hip_atomic_fetch_add(w, (unsigned long long)__double2ll_rn(t.x * FX_SCALE), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(w + BLOCK, (unsigned long long)__double2ll_rn(t.y * FX_SCALE), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(w + 2 * BLOCK, (unsigned long long)__double2ll_rn(t.z * FX_SCALE),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            __hip_atomic_fetch_add(mag, (float)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-            const double e[3] = {t.x, t.y, t.z};
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                w[k * BLOCK] = (unsigned long long)__double_as_longlong(
-                    __longlong_as_double((long long)w[k * BLOCK]) + e[k]);
-        }
-    }
-    __device__ __forceinline__ PixAcc load() const {
-        PixAcc a;
-        a.w[0] = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        a.w[1] = __hip_atomic_load(w + BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        a.w[2] = __hip_atomic_load(w + 2 * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        a.mag = __hip_atomic_load(mag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return a;
-    }
-};
-using PixAccT = PixAccLds;
-constexpr size_t PIX_LDS_BYTES = (size_t)BLOCK * 28;
-#else
-using PixAccT = PixAcc;
-constexpr size_t PIX_LDS_BYTES = 0;
-#endif
-#ifdef RT_COLD_LDS
-constexpr size_t COLD_LDS_BYTES = (size_t)BLOCK * 24;  // k_primary: xc, yr (f64), global pixel (u32) per thread
-#else
-constexpr size_t COLD_LDS_BYTES = 0;
-#endif
 
 // Emitter of the GPU trace step: colour -> framebuffer atomics, children -> output queue shard.
 struct GpuEmit {
@@ -370,7 +316,7 @@ struct GpuEmit {
     uint32_t shard;
     uint32_t round;
     uint32_t* shadow_acc;
-    PixAccT* acc;  // depth 0: the pixel's sums in the thread (no framebuffer atomics)
+    PixAcc* acc;  // depth 0: the pixel's sums in the thread (no framebuffer atomics)
 
     __device__ void local(d3 c) const {
         if (acc) {
@@ -641,7 +587,7 @@ struct FusedEmit {
     const Ray& r;
     uint32_t round;
     uint32_t* shadow_acc;
-    PixAccT* acc;
+    PixAcc* acc;
     Ray* next;
     bool* has;
 
@@ -707,21 +653,6 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
     const int s_begin = min(P.spp, grp * spg), s_end = min(P.spp, s_begin + spg);
     const int64_t nwaves = (P.npix + ppw - 1) / ppw;
     const Quot qw((double)P.cam.width), qh((double)P.cam.height);
-#ifdef RT_PIX_LDS
-    RT_LDS unsigned long long* pix_w =
-        (RT_LDS unsigned long long*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256) + threadIdx.x;
-    RT_LDS float* pix_mag = (RT_LDS float*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + 3 * BLOCK) + threadIdx.x;
-#endif
-#ifdef RT_COLD_LDS
-    // the item's per-pixel values read once per sample (camera grid coordinates, global pixel) kept in
-    // LDS instead of registers live across the trace: read back with relaxed atomic loads, which the
-    // compiler neither hoists nor keeps
-    RT_LDS double* cold_d = (RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + PIX_LDS_BYTES / 8 + threadIdx.x;
-    RT_LDS uint32_t* cold_u = (RT_LDS uint32_t*)((RT_LDS double*)rt_lds_dyn + P.S.nlut_lds * 256 + PIX_LDS_BYTES / 8 +
-                                                 2 * BLOCK) + threadIdx.x;
-#define COLD_D(k) __hip_atomic_load(cold_d + (k) * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-#define COLD_U(k) __hip_atomic_load(cold_u + (k) * BLOCK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-#endif
     for (int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); wv < nwaves;
          wv += (int64_t)gridDim.x * (BLOCK / 64)) {
         const int64_t p0 = wv * ppw;
@@ -731,24 +662,10 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
         const uint32_t lr = pact ? p / (uint32_t)P.cam.width : 0u;
         const uint32_t col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
         const int grow = pact ? P.rows[lr] : 0;
-#ifdef RT_COLD_LDS
-        cold_d[0] = pact ? P.cam.xs[col] : 0.0;
-        cold_d[BLOCK] = pact ? P.cam.ys[grow] : 0.0;
-        cold_u[0] = (uint32_t)grow * (uint32_t)P.cam.width + col;
-#define xc COLD_D(0)
-#define yr COLD_D(1)
-#define gpix COLD_U(0)
-#else
         const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
         const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
-#endif
         const int s_stop = active ? s_end : s_begin;  // (no samples for a lane past the frame's end)
-#ifdef RT_PIX_LDS
-        PixAccT acc{pix_w, pix_mag};
-        acc.zero();
-#else
         PixAcc acc;
-#endif
         // software pipeline: the next sample's pixel jitter is loaded while this sample is traced
         // (the lens-disk pair of a thin-lens camera is loaded when used: two fewer doubles live
         // across the trace for the pinhole cameras of every example)
@@ -791,17 +708,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
             }
             RT_ACC(3, tt0);
         }
-#ifdef RT_COLD_LDS
-#undef xc
-#undef yr
-#undef gpix
-#endif
         // the pixel's sample groups (lanes of this wave) summed; lane of group 0 stores the pixel
-#ifdef RT_PIX_LDS
-        PixAcc acc_r = acc.load();
-#else
         PixAcc& acc_r = acc;
-#endif
         acc_r.reduce_lanes(fx, ppw);
         const bool owner = pact && grp == 0;
         if (FUSE && P.fuse_resolve) {
@@ -3115,7 +3023,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
             hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
-                               lut_bytes(c) + PIX_LDS_BYTES + COLD_LDS_BYTES, c->f->stream, P);
+                               lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
             if (F.fuse)  // every depth traced: the deeper depths' events mark the same point
