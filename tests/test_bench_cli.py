@@ -95,3 +95,20 @@ def test_gpus_2_group_without_gpus_fails_without_a_line(tmp_path):
                        timeout=120)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_hw_queues_range_checked_and_exported(bench, monkeypatch, capsys):
+    """--hw-queues is set in the environment before HIP initialises (the boxes export 4) and is
+    range-checked (1..32)."""
+    monkeypatch.setattr(bench, "visible_gpus", lambda: 2)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--hw-queues", "40"])
+    with pytest.raises(SystemExit, match="hw-queues"):
+        bench.main()
+    seen = {}
+    monkeypatch.setattr(bench, "run_group", lambda args, gpus: seen.setdefault("q", os.environ["GPU_MAX_HW_QUEUES"]) and {})
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"])
+    bench.main()
+    assert seen == {"q": "7"}
