@@ -494,8 +494,6 @@ def main():
                          "frame in flight per hardware queue but one (rt_kernels.hip default_slots); 7 -> six "
                          "frames.  Set here, not inherited: the GPU boxes export HIP's default of 4, which "
                          "leaves four frame slots sharing three queues")
-    ap.add_argument("--cpu-node", type=int, default=-1,
-                    help="diagnostic: run this process on the CPUs of one NUMA node")
     ap.add_argument("--device-outputs", action="store_true",
                     help="diagnostic (one process): the frames' outputs left in HBM instead of host memory")
     ap.add_argument("--sync", action="store_true",
@@ -513,12 +511,6 @@ def main():
     ap.add_argument("--shard-snake", type=int, default=-1,
                     help="band dealing order, 0 round-robin / 1 snake (library option shard_snake; default SHARD_SNAKE)")
     args = ap.parse_args()
-    if args.cpu_node >= 0:  # (diagnostic: this process's threads on one NUMA node's CPUs)
-        cpus = set()
-        for part in open("/sys/devices/system/node/node%d/cpulist" % args.cpu_node).read().strip().split(","):
-            lo, _, hi = part.partition("-")
-            cpus.update(range(int(lo), int(hi or lo) + 1))
-        os.sched_setaffinity(0, cpus)
     if not 1 <= args.hw_queues <= 32:
         raise SystemExit("bench.py: --hw-queues 1 .. 32")
     os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)  # (before anything initialises HIP)
