@@ -1827,8 +1827,10 @@ uint32_t* mt_end_acc(srt_ctx* c) { return c->mt + MT_NTAB + 4 * rtmt::N; }
 uint32_t* mt_end_cnt(srt_ctx* c) { return c->mt + MT_NTAB + 5 * rtmt::N; }
 uint32_t* mt_ybuf(srt_ctx* c, int i) { return c->mt_y + (int64_t)i * MT_YBLOCKS * rtmt::N; }
 
-// Blocks per jump window (k_mt_jump parts): the option, else MT_MAX_PARTS
-int mt_jump_parts(const srt_ctx* c) { return c->mt_parts_opt ? c->mt_parts_opt : MT_MAX_PARTS; }
+// Blocks per jump window (k_mt_jump parts): the option, else 4 (final build, same box, against 8:
+// device-side whole frame 0.988 -> 0.979 ms, a rank of 8 0.204 -> 0.202, of 4 0.328 -> 0.318;
+// profiles/r04_jump_parts_ab.txt)
+int mt_jump_parts(const srt_ctx* c) { return c->mt_parts_opt ? c->mt_parts_opt : 4; }
 
 // The y words of `key` for a generation on `st`: those an end block made with the key (a final
 // window), else k_mt_y into the scratch buffer (one workgroup, ~34 blocks).  Generations of
