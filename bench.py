@@ -6,19 +6,23 @@ memory:
   * the camera jitter is the reference's numpy stream (np.random.seed(0) before the first frame,
     every frame continuing it, as consecutive Scene.render calls do), generated on the GPU inside the
     step (rt_mt.h; bit-equal to np.random.rand);
-  * every sample traced through every depth, the sRGB resolve;
-  * the uint8 image and the linear RGB (f64) copied to pinned host memory.
+  * every sample traced through every depth, the sRGB resolve: the linear RGB (f64) computed and
+    stored in HBM, the uint8 image copied to pinned host memory -- what Scene.render hands back (the
+    reference's render returns the uint8 image only, scene.py:118-140; SRT_RENDER_RGB_LOCAL).
 Frames are pipelined (each step queues its frame and returns; the timed region ends when all K
 frames are in host memory).  With N GPUs the library splits each frame into row bands dealt
 round-robin (SRT_RENDER_SHARDED), every rank draws the same stream and reads its rows, the uint8
-tiles are gathered to rank 0 over RCCL (xGMI) and every rank writes its rows of the linear RGB into
-the host frame over its own PCIe link; the frame is fixed, so scaling is strong.  Two launches, no
+tiles are gathered to rank 0 over RCCL (xGMI) and every rank keeps its rows of the linear RGB in its
+HBM; the frame is fixed, so scaling is strong.  `--rgb-to-host` copies the linear RGB to pinned host
+memory as well (rounds 1-4's step: 50 MB per 1080p frame over PCIe, every rank its own rows at
+N > 1); the default line reports that form too (`host_rgb`).  Two launches, no
 torch imported in either: one process per GPU (WORLD_SIZE set by a launcher such as the driver's
 `torch.distributed.run`; the ranks meet through the library's srt_comm_init), or -- `--gpus N` with no
 launcher -- this one process driving all N GPUs through the library's group (srt_comm_init_all +
 pipelined srt_render_group).
 
-Secondary figures in the same line: `frame_latency_ms` (one synchronous frame), `device_resident`
+Secondary figures in the same line: `host_rgb` (the same frames with the linear RGB copied to host
+memory too), `frame_latency_ms` (one synchronous frame), `device_resident`
 (jitter pre-resident in HBM and outputs left in HBM: the round-1 headline), the roofline of the
 dominant kernel, and the CPU baseline (oracle: one core, and a multiprocessing.Pool over samples
 structured like the reference's Scene.render).
@@ -411,11 +415,14 @@ def run_group(args, gpus):
     a.seed = 12345
     frame = {"k": 0}
 
-    def step(async_ok=True, st=None):
+    def step(async_ok=True, st=None, host_rgb=args.rgb_to_host):
         u8, rgb = outs[frame["k"] % NOUT]
         frame["k"] += 1
-        a.out_srgb8, a.out_rgb = u8, rgb
-        a.flags = (N.RENDER_ASYNC | N.RENDER_RGB_ROWS) if async_ok else 0
+        # host_rgb: every GPU writes its rows of the linear RGB into the pinned host frame (RGB_ROWS,
+        # pipelined frames) or rank 0 gathers it (synchronous); else every GPU keeps its rows in HBM
+        a.out_srgb8, a.out_rgb = u8, (rgb if host_rgb else None)
+        a.flags = ((N.RENDER_ASYNC | (N.RENDER_RGB_ROWS if host_rgb else 0)) if async_ok else 0) | \
+            (0 if host_rgb else N.RENDER_RGB_LOCAL)
         N.check(lib, lib.srt_render_group(ctxs, gpus, ctypes.byref(cd), ctypes.byref(a),
                                           ctypes.byref(st) if st is not None else None))
 
@@ -424,15 +431,18 @@ def run_group(args, gpus):
     N.check(lib, lib.srt_render_group_finish(ctxs, gpus, None))
     for c in ctx:
         N.check(lib, lib.srt_synchronize(c))
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(async_ok=not args.sync)
-    last = N.Stats()
-    N.check(lib, lib.srt_render_group_finish(ctxs, gpus, ctypes.byref(last)))  # every GPU's frames done
-    for c in ctx:
-        N.check(lib, lib.srt_synchronize(c))
-    el = time.perf_counter() - t0
-    last = last.as_dict()
+
+    def timed(host_rgb):
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(async_ok=not args.sync, host_rgb=host_rgb)
+        st = N.Stats()
+        N.check(lib, lib.srt_render_group_finish(ctxs, gpus, ctypes.byref(st)))  # every GPU's frames done
+        for c in ctx:
+            N.check(lib, lib.srt_synchronize(c))
+        return time.perf_counter() - t0, st.as_dict()
+
+    el, last = timed(args.rgb_to_host)
     ms_step = el / args.steps * 1e3
     rec = {
         "metric": "Mrays/sec (primary+secondary) + frame ms at 1920x1080 depth 5" if args.config == "example1_1080p_d5"
@@ -448,11 +458,13 @@ def run_group(args, gpus):
                    "shadow_rays": last["shadow_rays"], "kernel_path_rank0": last["kernel_path"],
                    "parallelism": "row-band shards x%d in one process (srt_comm_init_all + pipelined "
                                   "srt_render_group, no torch): uint8 tiles gathered to GPU 0 over RCCL (xGMI); every "
-                                  "GPU writes its rows of the linear RGB into the pinned host frame over its own PCIe "
-                                  "link" % gpus,
+                                  "GPU %s" % (gpus, "writes its rows of the linear RGB into the pinned host frame over "
+                                                    "its own PCIe link" if args.rgb_to_host else
+                                                    "keeps its rows of the linear RGB in its HBM"),
                    "frame": "render_group() entry (scene resident on every GPU) -> jitter stream on every GPU -> all "
-                            "samples and depths -> sRGB resolve -> gather -> uint8 + linear RGB (f64) in pinned host "
-                            "memory; frames pipelined",
+                            "samples and depths -> sRGB resolve -> gather -> uint8 image in pinned host memory, %s; "
+                            "frames pipelined" % ("linear RGB (f64) in pinned host memory too" if args.rgb_to_host
+                                                  else "every GPU's rows of the linear RGB (f64) stored in its HBM"),
                    "frame_ms": round(ms_step, 4),
                    "row_bands": {"kmax": shard_kmax(H, gpus, args.shard_bands, scene_fanout(sc)),
                                  "snake": args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE,
@@ -461,6 +473,12 @@ def run_group(args, gpus):
                                                             args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE)}},
     }
     if not args.no_secondary:
+        if not args.rgb_to_host:
+            el2, st2 = timed(True)
+            rec["host_rgb"] = {"value": round(st2["total_rays"] * args.steps / el2 / 1e6, 3),
+                               "ms_per_step": round(el2 / args.steps * 1e3, 4),
+                               "what": "same frames with every GPU's rows of the linear RGB copied into the pinned "
+                                       "host frame as well (SRT_RENDER_RGB_ROWS)"}
         lat = []
         for _ in range(3):
             t1 = time.perf_counter()
@@ -494,6 +512,9 @@ def main():
                          "frame in flight per hardware queue but one (rt_kernels.hip default_slots); 7 -> six "
                          "frames.  Set here, not inherited: the GPU boxes export HIP's default of 4, which "
                          "leaves four frame slots sharing three queues")
+    ap.add_argument("--rgb-to-host", action="store_true",
+                    help="headline frames copy the linear RGB (f64) to pinned host memory as well as the uint8 image "
+                         "(rounds 1-4's step); default: the uint8 image to host memory, the linear RGB kept in HBM")
     ap.add_argument("--device-outputs", action="store_true",
                     help="diagnostic (one process): the frames' outputs left in HBM instead of host memory")
     ap.add_argument("--sync", action="store_true",
@@ -565,7 +586,12 @@ def main():
     B.upload(sc)
     cd = B.camera_desc(sc.camera)
     npix_full = W * H
-    flags = N.RENDER_SHARDED | N.RENDER_RGB_ROWS if world > 1 else 0
+    # the linear RGB: host memory (--rgb-to-host: every rank its own rows over its PCIe link at N > 1)
+    # or each rank's rows kept in its HBM (SRT_RENDER_RGB_LOCAL)
+    base_flags = N.RENDER_SHARDED if world > 1 else 0
+
+    def frame_flags(host_rgb):
+        return base_flags | ((N.RENDER_RGB_ROWS if world > 1 else 0) if host_rgb else N.RENDER_RGB_LOCAL)
     rows32 = None
     from sightpy._shard import SHARD_SNAKE, band_height, scene_fanout, shard_kmax, shard_rows
 
@@ -613,11 +639,11 @@ def main():
     a.out_hit_id = None
     frame = {"k": 0}
 
-    def step(async_ok=True, st=None):
+    def step(async_ok=True, st=None, host_rgb=args.rgb_to_host):
         u8, rgb = outs[frame["k"] % NOUT]
-        a.out_srgb8, a.out_rgb = (u8 if u8.value else None), rgb
+        a.out_srgb8, a.out_rgb = (u8 if u8.value else None), (rgb if host_rgb else None)
         frame["k"] += 1
-        a.flags = flags | (N.RENDER_ASYNC if async_ok else 0)
+        a.flags = frame_flags(host_rgb) | (N.RENDER_ASYNC if async_ok else 0)
         N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st) if st else None))
 
     def barrier():
@@ -625,6 +651,18 @@ def main():
         N.check(lib, lib.srt_synchronize(ctx))
         if world > 1:
             N.check(lib, lib.srt_comm_barrier(ctx))
+
+    def timed(host_rgb):
+        """args.steps pipelined frames after a barrier: (seconds, last frame's stats)"""
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(async_ok=not args.sync, host_rgb=host_rgb)
+        enq_ms = (time.perf_counter() - t0) / args.steps * 1e3  # host time to queue a frame
+        st = N.Stats()
+        N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(st)))  # every frame in host memory, flags checked
+        if world > 1:
+            N.check(lib, lib.srt_comm_barrier(ctx))
+        return time.perf_counter() - t0, st.as_dict(), enq_ms
 
     rank_ms, rank_rays, enq = [], [], []
     for i, (rr, rows_r) in enumerate(rehearse.items()):
@@ -642,16 +680,8 @@ def main():
             if w % 50 == 0:
                 barrier()  # (bounded queue depth while priming)
         barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step(async_ok=not args.sync)
-        enq.append((time.perf_counter() - t0) / args.steps * 1e3)  # host time to queue a frame
-        last = N.Stats()
-        N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(last)))  # every frame in host memory, flags checked
-        if world > 1:
-            N.check(lib, lib.srt_comm_barrier(ctx))
-        el = time.perf_counter() - t0
-        last = last.as_dict()
+        el, last, enq_ms = timed(args.rgb_to_host)
+        enq.append(enq_ms)
         rank_ms.append(el / args.steps * 1e3)
         rank_rays.append(last["total_rays"])
     elapsed = max(rank_ms) * args.steps / 1e3
@@ -670,6 +700,18 @@ def main():
 
     # ---- secondary figures --------------------------------------------------------------------
     sec = {}
+    if not args.no_secondary and not args.rgb_to_host and not args.device_outputs and len(rehearse) == 1:
+        # the same frames with the linear RGB copied to host memory as well (rounds 1-4's step)
+        barrier()
+        el2, st2, _ = timed(True)
+        vals2 = (ctypes.c_double * 1)(el2)
+        if world > 1:
+            N.check(lib, lib.srt_comm_allreduce(ctx, vals2, 1, 1))
+        sec["host_rgb"] = {"value": round(total_rays * args.steps / vals2[0] / 1e6, 3),
+                           "ms_per_step": round(vals2[0] / args.steps * 1e3, 4),
+                           "what": "same frames with the linear RGB (f64) copied to pinned host memory as well "
+                                   "(%s)" % ("every rank its rows into the shared host frame, SRT_RENDER_RGB_ROWS"
+                                             if world > 1 else "50 MB per 1080p frame over one PCIe link")}
     if not args.no_secondary:
         # one synchronous frame, render() entry -> host memory (latency, not throughput)
         lat = []
@@ -734,15 +776,19 @@ def main():
                        "shadow_rays_rank0": last["shadow_rays"], "kernel_path": last["kernel_path"],
                        "chain_from_depth": last["chain_from"],
                        "parallelism": "row-band shards x%d: uint8 tiles gathered to rank 0 over RCCL (xGMI); every rank "
-                                      "writes its rows of the linear RGB into the shared host frame over its own "
-                                      "PCIe link" % world
+                                      "%s" % (world, "writes its rows of the linear RGB into the shared host frame over "
+                                                     "its own PCIe link" if args.rgb_to_host else
+                                                     "keeps its rows of the linear RGB in its HBM")
                        if world > 1 else (("diagnostic: rank %s's rows of a %d-rank job, no gather" % (
                                               args.shard_rank, args.shard_of) if len(rehearse) == 1 else
                                               "diagnostic: every rank's rows of a %d-rank job rendered in turn on "
                                               "one GPU, no gather; ms_per_step = the slowest rank's frame"
                                               % args.shard_of) if rows32 is not None else "1 GPU"),
                        "frame": "render() entry (scene resident) -> jitter stream on the GPU -> all samples and depths "
-                                "-> sRGB resolve -> uint8 + linear RGB (f64) in pinned host memory; frames pipelined",
+                                "-> sRGB resolve -> uint8 image in pinned host memory, %s; frames pipelined"
+                                % ("linear RGB (f64) in pinned host memory too" if args.rgb_to_host else
+                                   "the linear RGB (f64) stored in HBM (what Scene.render keeps; the reference "
+                                   "returns the uint8 image, scene.py:118-140)"),
                        "frame_ms": round(ms_step, 4),
                        "host_enqueue_ms": round(max(enq), 4),
                        "row_bands": {"kmax": kmax, "snake": snake,
@@ -753,7 +799,9 @@ def main():
             rec["rank_frame_ms"] = [round(rank_ms[order.index(r)], 4) for r in sorted(order)]
             rec["rank_rays"] = [rank_rays[order.index(r)] for r in sorted(order)]
             rec["rehearsal_order"] = order
-        if sec:
+        if "host_rgb" in sec:
+            rec["host_rgb"] = sec["host_rgb"]
+        if "frame_latency_ms" in sec:
             rec["config"]["frame_latency_ms"] = sec["frame_latency_ms"]
             if "device_resident" in sec:
                 rec["device_resident"] = sec["device_resident"]

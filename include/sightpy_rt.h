@@ -241,8 +241,9 @@ typedef struct srt_render_args {
  * create_animation and the multi-GPU frame loop.) */
 #define SRT_RENDER_ASYNC 1
 /* SRT_RENDER_SHARDED: the context's communicator (srt_comm_init / srt_comm_init_all) splits the
- * frame: this rank renders the rows {y : (y / 8) % nranks == rank} (8-row bands dealt round-robin,
- * which balances cheap sky rows against reflective floor rows; rows / n_rows are ignored) and the
+ * frame: this rank renders the rows {y : (y / h) % nranks == rank} (h-row bands dealt round-robin,
+ * which balances cheap sky rows against reflective floor rows; h = shard_band_height in rt_device.h,
+ * at most 8 bands per rank; rows / n_rows are ignored) and the
  * uint8 and linear-RGB tiles are gathered over RCCL to rank 0, whose out_srgb8 / out_rgb receive the
  * whole frame ([height][width][3], [3][height*width]); the other ranks' outputs are not written.
  * Replaces the reference's multiprocessing.Pool over samples (scene.py:80-116). */
@@ -255,6 +256,11 @@ typedef struct srt_render_args {
  * each over its own PCIe link; the RCCL gather to rank 0 then carries only the uint8 image.  The
  * frame's linear RGB is complete in host memory when every rank's frame has finished. */
 #define SRT_RENDER_RGB_ROWS 8
+/* SRT_RENDER_RGB_LOCAL (out_rgb NULL, without GATHER_RGB / RGB_ROWS): the linear RGB of the rows this
+ * call renders is resolved into the context's frame buffer in HBM and stays there -- what
+ * Scene.render keeps (the reference returns only the uint8 image, scene.py:118-140): the whole RGB
+ * is computed and stored, nothing crosses PCIe or xGMI but the uint8 image. */
+#define SRT_RENDER_RGB_LOCAL 16
 
 #define SRT_MAX_DEPTHS 64
 typedef struct srt_stats {
@@ -360,8 +366,9 @@ int srt_comm_rank(srt_ctx* ctx, int* nranks, int* rank);
  * receive the frame), stats of rank 0 plus total_rays / rays_per_depth / shadow_rays summed.
  * args->flags may hold SRT_RENDER_ASYNC (queue the frame on every context, gather posted, return at
  * once; outputs in pinned host memory from srt_host_alloc; `stats` not written; finish with
- * srt_render_group_finish) and SRT_RENDER_RGB_ROWS (with ASYNC: every context writes its rows of the
- * linear RGB into out_rgb over its own PCIe link instead of the RCCL gather to rank 0). */
+ * srt_render_group_finish), SRT_RENDER_RGB_ROWS (with ASYNC: every context writes its rows of the
+ * linear RGB into out_rgb over its own PCIe link instead of the RCCL gather to rank 0) and
+ * SRT_RENDER_RGB_LOCAL (out_rgb NULL: every context keeps its rows of the linear RGB in its HBM). */
 int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);
 /* wait for the group's asynchronous frames: errors of every context, the last frame's stats summed as
  * srt_render_group returns them */

@@ -488,9 +488,15 @@ RT_HD const RT_RO uint8_t* tex_uv(const SceneView& S, const RT_RO srt_texture& T
 // The three bytes of a texel through the texture's table.  A 4-byte texel read from its first byte
 // (RGBX: srt_upload_scene stores 3-channel images that way, and RGBA images are) is one aligned
 // dword load instead of three byte loads; other layouts read the bytes.
+// A texture whose texels can be read as one dword each: 4 channels from the first, and the image
+// 4-byte aligned in the pool (srt_upload_scene pads the RGBX pool so; a caller's own pool or offsets
+// may not be).  Wave-uniform: scalar operations on the texture record.
+RT_HD bool texel_dword(const SceneView& S, const RT_RO srt_texture& T) {
+    return T.channels == 4 && T.channel0 == 0 && (((uintptr_t)S.texels + (uint64_t)T.offset) & 3u) == 0;
+}
 RT_HD d3 texel_rgb(const SceneView& S, const RT_RO srt_texture& T, int tid, const RT_RO uint8_t* px) {
     uint32_t b0, b1, b2;
-    if (T.channels == 4 && T.channel0 == 0) {
+    if (texel_dword(S, T)) {
         const uint32_t w = *reinterpret_cast<const RT_RO uint32_t*>(px);
         b0 = w & 0xFFu;
         b1 = (w >> 8) & 0xFFu;
@@ -511,8 +517,8 @@ RT_HD d3 tex_rgb(const SceneView& S, int tid, double u, double v, uint32_t& err)
 }
 
 // A texel's 4 bytes as one word (texel_rgb's layouts): one dword load for RGBX / RGBA texels
-RT_HD uint32_t texel_word(const RT_RO srt_texture& T, const RT_RO uint8_t* px) {
-    if (T.channels == 4 && T.channel0 == 0) return *reinterpret_cast<const RT_RO uint32_t*>(px);
+RT_HD uint32_t texel_word(const SceneView& S, const RT_RO srt_texture& T, const RT_RO uint8_t* px) {
+    if (texel_dword(S, T)) return *reinterpret_cast<const RT_RO uint32_t*>(px);
     return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
 }
 RT_HD d3 word_rgb(const SceneView& S, int tid, uint32_t w) {
@@ -669,7 +675,11 @@ RT_HD uint64_t bvh_entry(double tn, int32_t code) {
     return ((uint64_t)bvh_f2u(f) << 32) | (uint32_t)code;
 }
 RT_HD int32_t bvh_code(int32_t child, int32_t count) {
-    return child >= 0 ? child : -(1 + (((-child - 1) << 6) | count));
+    // (the negation in uint32_t: defined for every input, BVH_EMPTY included, though callers pass it
+    // only non-empty children)
+    if (child >= 0) return child;
+    const uint32_t leaf = (0u - (uint32_t)child) - 1u;
+    return (int32_t)(0u - (1u + ((leaf << 6) | (uint32_t)count)));
 }
 
 // The four children of a node against the ray: entry distances t[k] (INFINITY: missed, empty, or
@@ -678,7 +688,7 @@ RT_HD void bvh_children(const RT_RO BvhNode& nd, d3 O, d3 inv, double limit, boo
                         int32_t c[4]) {
 RT_UNROLL
     for (int k = 0; k < 4; ++k) {
-        c[k] = bvh_code(nd.child[k], nd.count[k]);
+        c[k] = nd.child[k] == BVH_EMPTY ? BVH_EMPTY : bvh_code(nd.child[k], nd.count[k]);
         double tn;
         const bool hit = nd.child[k] != BVH_EMPTY && box4_hit(nd, k, O, inv, tn) && (strict ? tn < limit : tn <= limit);
         t[k] = hit ? tn : INFINITY;
@@ -926,7 +936,7 @@ RT_HD void shade_glossy(const SceneView& S, const RT_RO srt_collider& c, int mi,
     if (m.tex >= 0) {
         double u, v;
         if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
-        tw = texel_word(S.tex[m.tex], tex_uv(S, S.tex[m.tex], u, v, err));
+        tw = texel_word(S, S.tex[m.tex], tex_uv(S, S.tex[m.tex], u, v, err));
     }
     RT_ACC(4, tg0);
     RT_T0(tg1);
@@ -1151,10 +1161,10 @@ RT_HD void sky_fetch(const SceneView& S, const Ray& r, double t, uint32_t& w0, u
     const d3 P = add(r.o, mul(r.d, t));
     double u, v;
     if (!collider_uv(c, P, u, v)) err |= ERR_UNSUPPORTED;
-    w0 = texel_word(S.tex[m.tex], tex_uv(S, S.tex[m.tex], u, v, err));
+    w0 = texel_word(S, S.tex[m.tex], tex_uv(S, S.tex[m.tex], u, v, err));
     w1 = 0u;
     if (meta_depth(r.meta) != 0 && (m.flags & SRT_MF_LIGHTMAP))
-        w1 = texel_word(S.tex[m.tex_aux0], tex_uv(S, S.tex[m.tex_aux0], u, v, err));
+        w1 = texel_word(S, S.tex[m.tex_aux0], tex_uv(S, S.tex[m.tex_aux0], u, v, err));
 }
 RT_HD d3 sky_color(const SceneView& S, const Ray& r, uint32_t w0, uint32_t w1) {
     const RT_RO srt_material& m = S.mat[S.col[S.sky_col].material];

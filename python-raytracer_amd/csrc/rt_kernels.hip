@@ -1083,13 +1083,14 @@ struct Variant {
     void (*chain)(TraceParams);
     void (*fused)(TraceParams) = nullptr;  // k_primary<.., FUSE>: whole single-child paths per pixel
 };
-// occupancy experiments for the headline scene (srt_set_option "occupancy" = 2 (1 wave/SIMD), 3, 4;
-// built with -DRT_OCC_VARIANTS); the default instantiations use RT_OCC = 3 waves/SIMD.  Same-box A/B
+// occupancy experiments for the headline scene (srt_set_option "occupancy" = k in 2..4 selects the
+// build for k waves/SIMD, OCC_VARIANTS[k - 2]; built with -DRT_OCC_VARIANTS); the default
+// instantiations use RT_OCC = 3 waves/SIMD.  Same-box A/B
 // against 2 waves/SIMD (profiles/r03_occ_ab.txt): device-resident ex1 1080p 1.22 -> 1.10 ms, ex3
 // k_frame 3.36 -> 3.06 ms, ex4 4K 14.5 -> 13.2 ms, cornell 4.87 -> 4.05 s, mesh 12.2 -> 10.2 ms.
 #ifdef RT_OCC_VARIANTS
 const Variant OCC_VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1>, k_frame<MATS_GLOSSY_SKY, 1>, k_trace<MATS_GLOSSY_SKY, 1, true>},
+    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 2>, k_trace<MATS_GLOSSY_SKY, 2>, k_frame<MATS_GLOSSY_SKY, 2>, k_trace<MATS_GLOSSY_SKY, 2, true>},
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>, k_frame<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3, true>},
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>, k_frame<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4, true>},
 };
@@ -1100,7 +1101,7 @@ int g_occupancy = 0;
 #endif
 constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (register cap 512 / OCC)
 #ifndef RT_FUSE_OCC
-#define RT_FUSE_OCC 3  // waves/SIMD of the fused k_primary (the child written over the ray: 10 VGPRs spilled)
+#define RT_FUSE_OCC 3  // waves/SIMD of the fused k_primary (168 VGPRs; its spills: DESIGN.md §3)
 #endif
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
@@ -1355,6 +1356,24 @@ hipError_t dalloc(T** p, int64_t count) {
     return hipMalloc((void**)p, (size_t)std::max<int64_t>(count, 1) * sizeof(T));
 }
 
+// Device buffers of one API call, freed on every exit path (the early HIP_TRY returns included)
+struct CallBufs {
+    std::vector<void*> p;
+    CallBufs() = default;
+    CallBufs(const CallBufs&) = delete;
+    CallBufs& operator=(const CallBufs&) = delete;
+    ~CallBufs() {
+        for (void* b : p) (void)hipFree(b);
+    }
+    template <typename T>
+    hipError_t alloc(T** out, int64_t count) {
+        *out = nullptr;
+        const hipError_t e = dalloc(out, count);
+        if (e == hipSuccess) p.push_back(*out);
+        return e;
+    }
+};
+
 int grid_for(int64_t n, int max_blocks) {
     int64_t b = (n + BLOCK - 1) / BLOCK;
     if (b < 1) b = 1;
@@ -1485,6 +1504,7 @@ struct srt_ctx {
     uint8_t* texels = nullptr;
     uint64_t texel_key = 0;
     int64_t texel_bytes = 0;
+    uint64_t texel_layout = 0;  // hash of the pool layout the records' offsets were remapped to
     bool texels_rgbx = false;  // the resident pool holds 3-channel images as RGBX
     bool texel_rgbx = true;    // option "texel_rgbx": store 3-channel images as RGBX (one dword per texel)
     bool sky_prefetch = true;  // option "sky_prefetch" (next srt_upload_scene): trace_one's early sky texel fetch
@@ -1564,6 +1584,10 @@ struct srt_ctx {
     int mt_pos = 0;
     hipEvent_t mt_done = nullptr;  // recorded after the last frame's stream generation
     int mt_cur = 0;                // which of the two final-window buffers is current (mt_dump)
+    // a generation stopped between its jump and its generator launches (an error return) leaves
+    // windows that are not zero and possibly a partial end accumulator: every slot's window table,
+    // end_acc and end_cnt are cleared before the next generation (mt_win_ensure)
+    bool mt_dirty = false;
     // single-pass frames generate their numpy stream on a stream of their own, so the generation of
     // frame k+1 runs beside frame k's trace (their order is this stream's order)
     hipStream_t mt_stream = nullptr;
@@ -1662,12 +1686,23 @@ int ensure_buf(T** p, int64_t& cap, int64_t count) {
 }
 
 // The segment-window table of a slot's numpy-stream generation: zero when (re)allocated; from then
-// on every window a jump XORs into is zeroed again by the generator that reads it
-int mt_win_ensure(uint32_t** p, int64_t& cap, int64_t count) {
-    if (count <= cap && *p) return SRT_OK;
-    int rc = ensure_buf(p, cap, count);
+// on every window a jump XORs into is zeroed again by the generator that reads it.  After a
+// generation that stopped between its jump and generator launches (srt_ctx::mt_dirty) every slot's
+// table and the end accumulator are cleared first (device-synchronous: an error path only).
+int mt_end_reset(srt_ctx* c);
+int mt_win_ensure(srt_ctx* c, FrameSlot& f, int64_t count) {
+    if (c->mt_dirty) {
+        HIP_TRY(hipDeviceSynchronize());
+        for (FrameSlot& s : c->slots)
+            if (s.mt_win) HIP_TRY(hipMemset(s.mt_win, 0, (size_t)s.mt_win_cap * 4));
+        int rc = mt_end_reset(c);
+        if (rc) return rc;
+        c->mt_dirty = false;
+    }
+    if (count <= f.mt_win_cap && f.mt_win) return SRT_OK;
+    int rc = ensure_buf(&f.mt_win, f.mt_win_cap, count);
     if (rc) return rc;
-    HIP_TRY(hipMemset(*p, 0, (size_t)count * 4));
+    HIP_TRY(hipMemset(f.mt_win, 0, (size_t)count * 4));
     return SRT_OK;
 }
 
@@ -1826,6 +1861,10 @@ uint32_t* mt_dump_at(srt_ctx* c, int d) { return c->mt + MT_NTAB + (2 + d) * rtm
 uint32_t* mt_end_acc(srt_ctx* c) { return c->mt + MT_NTAB + 4 * rtmt::N; }
 uint32_t* mt_end_cnt(srt_ctx* c) { return c->mt + MT_NTAB + 5 * rtmt::N; }
 uint32_t* mt_ybuf(srt_ctx* c, int i) { return c->mt_y + (int64_t)i * MT_YBLOCKS * rtmt::N; }
+int mt_end_reset(srt_ctx* c) {
+    if (c->mt) HIP_TRY(hipMemset(mt_end_acc(c), 0, (rtmt::N + 1) * 4));  // end_acc [624] and end_cnt [1]
+    return SRT_OK;
+}
 
 // Blocks per jump window (k_mt_jump parts): the option, else 4 (final build, same box, against 8:
 // device-side whole frame 0.988 -> 0.979 ms, a rank of 8 0.204 -> 0.202, of 4 0.328 -> 0.318;
@@ -1981,6 +2020,7 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     A.parts = mt_jump_parts(c);
     // the segment windows are XOR-accumulated by their jump parts into the table, which is zero here:
     // zeroed when allocated (mt_win_ensure), and every generator zeroes the window it read
+    c->mt_dirty = true;  // (until the generators that zero the windows are queued)
     hipLaunchKernelGGL(k_mt_jump, dim3((T.nseg + 1) * A.parts), dim3(MT_THREADS), mt_jump_lds_bytes(A.parts), st, A,
                        win);
     HIP_TRY(hipGetLastError());
@@ -1990,6 +2030,7 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     G.y_next = nullptr;
     hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
     HIP_TRY(hipGetLastError());
+    c->mt_dirty = false;
     c->mt_y_valid[c->mt_cur ^ 1] = true;
     c->mt_cur ^= 1;
     *final_pos = (int)(abs_end - dump_abs);
@@ -2039,6 +2080,7 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
             c->mt_y_valid[c->mt_cur ^ 1] = end;  // (a generator segment makes the window, not its y)
         }
         if (jump_blocks > 0) {
+            c->mt_dirty = true;  // (until the generators that zero the windows are queued)
             A.y = mt_y_for(c, st, A.key);
             A.end_acc = mt_end_acc(c);
             A.end_cnt = mt_end_cnt(c);
@@ -2055,6 +2097,7 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
         if (end) G.dump_dst = nullptr;  // (made by the jump kernel)
         hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
         HIP_TRY(hipGetLastError());
+        c->mt_dirty = false;
     }
     c->mt_cur ^= 1;
     *final_pos = plan.final_pos;
@@ -2513,9 +2556,18 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
                 }
     }
     if ((rc = upload(c, tex_h.data(), d->n_textures, &tex))) return rc;
-    // kept in HBM across uploads while the caller's key and size (and the layout) are unchanged
+    // the pool's layout: the images (caller offset, bytes, pool offset, expanded) it holds, or the
+    // caller's pool as given -- a key reused with another image set must not reuse the pool
+    uint64_t layout = 1469598103934665603ull;
+    auto mix = [&layout](int64_t v) { layout = (layout ^ (uint64_t)v) * 1099511628211ull; };
+    mix(pool_bytes);
+    mix(rgbx);
+    if (rgbx)
+        for (const auto& im : imgs)
+            for (int64_t v : im) mix(v);
+    // kept in HBM across uploads while the caller's key and size and the layout are unchanged
     if (d->texel_key != 0 && d->texel_key == c->texel_key && d->texel_bytes == c->texel_bytes && c->texels &&
-        rgbx == c->texels_rgbx) {
+        rgbx == c->texels_rgbx && layout == c->texel_layout) {
         texels = c->texels;
     } else {
         if (c->texels) (void)hipFree(c->texels);
@@ -2544,6 +2596,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
             c->texel_key = d->texel_key;
             c->texel_bytes = d->texel_bytes;
             c->texels_rgbx = rgbx;
+            c->texel_layout = layout;
         }
     }
     if ((rc = upload(c, d->lights, d->n_lights, &lights))) return rc;
@@ -2615,8 +2668,11 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
-    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS))
+    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS |
+                     SRT_RENDER_RGB_LOCAL))
         return fail(SRT_ERR_ARG, "unknown render flag");
+    if ((a->flags & SRT_RENDER_RGB_LOCAL) && (a->out_rgb || (a->flags & (SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS))))
+        return fail(SRT_ERR_ARG, "SRT_RENDER_RGB_LOCAL needs out_rgb NULL and no SRT_RENDER_GATHER_RGB / RGB_ROWS");
     if ((a->flags & SRT_RENDER_RGB_ROWS) &&
         (!(a->flags & SRT_RENDER_SHARDED) || (a->flags & SRT_RENDER_GATHER_RGB) || !a->out_rgb))
         return fail(SRT_ERR_ARG, "SRT_RENDER_RGB_ROWS needs SRT_RENDER_SHARDED, out_rgb and no SRT_RENDER_GATHER_RGB");
@@ -2764,7 +2820,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         const bool same = W <= c->cam_cap[0] && cam->height <= c->cam_cap[1] && n_rows <= c->cam_cap[2] &&
                           3 * npix <= c->f->fb_cap && fx_words(npix) <= c->f->fbx_cap && 3 * npix <= c->f->rgb_cap &&
                           3 * npix <= c->f->u8_cap &&
-                          jit_doubles <= c->f->jit_cap && (!use_mt || mt_win_need <= c->f->mt_win_cap) &&
+                          jit_doubles <= c->f->jit_cap && (!use_mt || (mt_win_need <= c->f->mt_win_cap && !c->mt_dirty)) &&
                           (F.frame || (int64_t)batch * npix * c->fanout <= c->f->seg * NSHARD) &&
                           (!F.frame || c->f->ring_cap > 0) && F.npass == pp.npass && F.dcap == pp.dcap &&
                           F.frame == pp.frame && F.chain_from == pp.chain_from && F.fuse == pp.fuse && F.W == pp.W && F.H == pp.H &&
@@ -2806,7 +2862,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!r) r = ensure_buf(&c->f->rgb, c->f->rgb_cap, 3 * npix);
         if (!r) r = ensure_buf(&c->f->u8, c->f->u8_cap, 3 * npix);
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
-        if (!r && use_mt) r = mt_win_ensure(&c->f->mt_win, c->f->mt_win_cap, mt_win_need);
+        if (!r && use_mt) r = mt_win_ensure(c, *c->f, mt_win_need);
         if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
         if (!r && sharded && c->rank == 0) {
             r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, c->nranks * maxpix * 3);
@@ -2856,7 +2912,9 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // for the ex1 1080p RGB, against 28 GB/s for a resolve kernel storing straight into pinned
     // memory over PCIe); a shard resolves into its slot tiles (gathered afterwards)
     const bool rgb_direct = rk == 1, u8_direct = uk == 1;
-    double* res_rgb = sharded ? ((gather_rgb || rgb_rows) ? c->f->rgb : nullptr)
+    const bool rgb_local = (a->flags & SRT_RENDER_RGB_LOCAL) != 0;
+    double* res_rgb = rgb_local ? c->f->rgb
+                    : sharded ? ((gather_rgb || rgb_rows) ? c->f->rgb : nullptr)
                               : a->out_rgb ? (rgb_direct ? a->out_rgb : c->f->rgb) : nullptr;
     uint8_t* res_u8 = sharded ? c->f->u8 : a->out_srgb8 ? (u8_direct ? a->out_srgb8 : c->f->u8) : nullptr;
     // only the depths this frame can reach are handed back and cleared per pass
@@ -3227,20 +3285,21 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
     c->f->dirty = true;  // counts/flags/shadow are left as this call's memsets and kernels leave them
     const int64_t n = a->n;
     int rc = SRT_OK;
+    CallBufs bufs;  // (freed on every return)
     double *O = nullptr, *D = nullptr;
     int32_t* med = nullptr;
-    HIP_TRY(dalloc(&O, 3 * n));
-    HIP_TRY(dalloc(&D, 3 * n));
-    if (a->medium) HIP_TRY(dalloc(&med, n));
+    HIP_TRY(bufs.alloc(&O, 3 * n));
+    HIP_TRY(bufs.alloc(&D, 3 * n));
+    if (a->medium) HIP_TRY(bufs.alloc(&med, n));
     HIP_TRY(hipMemcpyAsync(O, a->origin, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
     HIP_TRY(hipMemcpyAsync(D, a->dir, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
     if (med) HIP_TRY(hipMemcpyAsync(med, a->medium, (size_t)n * 4, hipMemcpyDefault, c->f->stream));
     int32_t* dfid = nullptr;
     double *dft = nullptr, *dfo = nullptr;
     if (fid) {
-        HIP_TRY(dalloc(&dfid, n));
-        HIP_TRY(dalloc(&dft, n));
-        HIP_TRY(dalloc(&dfo, n));
+        HIP_TRY(bufs.alloc(&dfid, n));
+        HIP_TRY(bufs.alloc(&dft, n));
+        HIP_TRY(bufs.alloc(&dfo, n));
         HIP_TRY(hipMemcpyAsync(dfid, fid, (size_t)n * 4, hipMemcpyDefault, c->f->stream));
         HIP_TRY(hipMemcpyAsync(dft, ft, (size_t)n * 8, hipMemcpyDefault, c->f->stream));
         HIP_TRY(hipMemcpyAsync(dfo, fo, (size_t)n * 8, hipMemcpyDefault, c->f->stream));
@@ -3329,12 +3388,6 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
         HIP_TRY(hipStreamSynchronize(c->f->stream));
         break;
     }
-    (void)hipFree(O);
-    (void)hipFree(D);
-    if (med) (void)hipFree(med);
-    void* fb_[] = {dfid, dft, dfo};
-    for (void* b : fb_)
-        if (b) (void)hipFree(b);
     if (rc) return rc;
     S.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     if (st) *st = S;
@@ -3359,13 +3412,14 @@ int srt_nearest(srt_ctx* c, const double* O, const double* D, int64_t n, double*
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
     if (n <= 0) return SRT_OK;
     HIP_TRY(hipSetDevice(c->device));
+    CallBufs bufs;
     double *dO, *dD, *dt, *dor;
     int32_t* did;
-    HIP_TRY(dalloc(&dO, 3 * n));
-    HIP_TRY(dalloc(&dD, 3 * n));
-    HIP_TRY(dalloc(&dt, n));
-    HIP_TRY(dalloc(&dor, n));
-    HIP_TRY(dalloc(&did, n));
+    HIP_TRY(bufs.alloc(&dO, 3 * n));
+    HIP_TRY(bufs.alloc(&dD, 3 * n));
+    HIP_TRY(bufs.alloc(&dt, n));
+    HIP_TRY(bufs.alloc(&dor, n));
+    HIP_TRY(bufs.alloc(&did, n));
     HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
     hipLaunchKernelGGL(k_nearest, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->S, dO, dD, n, dt, did,
@@ -3375,8 +3429,6 @@ int srt_nearest(srt_ctx* c, const double* O, const double* D, int64_t n, double*
     if (t) HIP_TRY(hipMemcpy(t, dt, (size_t)n * 8, hipMemcpyDefault));
     if (id) HIP_TRY(hipMemcpy(id, did, (size_t)n * 4, hipMemcpyDefault));
     if (orient) HIP_TRY(hipMemcpy(orient, dor, (size_t)n * 8, hipMemcpyDefault));
-    void* bufs[] = {dO, dD, dt, dor, did};
-    for (void* p : bufs) (void)hipFree(p);
     return SRT_OK;
 }
 
@@ -3386,12 +3438,13 @@ int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O,
     if (col->type < 0 || col->type > 3) return fail(SRT_ERR_ARG, "bad collider type");
     if (n <= 0) return SRT_OK;
     HIP_TRY(hipSetDevice(c->device));
+    CallBufs bufs;
     double *dO, *dD, *dout;
     srt_collider* dcol;
-    HIP_TRY(dalloc(&dO, 3 * n));
-    HIP_TRY(dalloc(&dD, 3 * n));
-    HIP_TRY(dalloc(&dout, 2 * n));
-    HIP_TRY(dalloc(&dcol, 1));
+    HIP_TRY(bufs.alloc(&dO, 3 * n));
+    HIP_TRY(bufs.alloc(&dD, 3 * n));
+    HIP_TRY(bufs.alloc(&dout, 2 * n));
+    HIP_TRY(bufs.alloc(&dcol, 1));
     HIP_TRY(hipMemcpy(dO, O, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dD, D, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dcol, col, sizeof(srt_collider), hipMemcpyDefault));
@@ -3400,10 +3453,6 @@ int srt_intersect_collider(srt_ctx* c, const srt_collider* col, const double* O,
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->f->stream));
     HIP_TRY(hipMemcpy(out, dout, (size_t)2 * n * 8, hipMemcpyDefault));
-    (void)hipFree(dcol);
-    (void)hipFree(dO);
-    (void)hipFree(dD);
-    (void)hipFree(dout);
     return SRT_OK;
 }
 
@@ -3415,14 +3464,15 @@ int srt_collider_surface(srt_ctx* c, const srt_collider* col, const double* P, i
         return fail(SRT_ERR_ARG, "Triangle uv is undefined in the reference (triangle.py:79-83)");
     if (n <= 0) return SRT_OK;
     HIP_TRY(hipSetDevice(c->device));
+    CallBufs bufs;
     srt_collider rec = *col;
     if (!primitive_uv) rec.flags &= ~SRT_CF_UV_CROSS;  // the collider's own 4x3 cross coordinates
     double *dP, *dN = nullptr, *duv = nullptr;
     srt_collider* dcol;
-    HIP_TRY(dalloc(&dP, 3 * n));
-    if (N) HIP_TRY(dalloc(&dN, 3 * n));
-    if (uv) HIP_TRY(dalloc(&duv, 2 * n));
-    HIP_TRY(dalloc(&dcol, 1));
+    HIP_TRY(bufs.alloc(&dP, 3 * n));
+    if (N) HIP_TRY(bufs.alloc(&dN, 3 * n));
+    if (uv) HIP_TRY(bufs.alloc(&duv, 2 * n));
+    HIP_TRY(bufs.alloc(&dcol, 1));
     HIP_TRY(hipMemcpy(dP, P, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dcol, &rec, sizeof(srt_collider), hipMemcpyDefault));
     hipLaunchKernelGGL(k_collider_surface, dim3(grid_for(n, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, dcol, dP, n,
@@ -3431,9 +3481,6 @@ int srt_collider_surface(srt_ctx* c, const srt_collider* col, const double* P, i
     HIP_TRY(hipStreamSynchronize(c->f->stream));
     if (N) HIP_TRY(hipMemcpy(N, dN, (size_t)3 * n * 8, hipMemcpyDefault));
     if (uv) HIP_TRY(hipMemcpy(uv, duv, (size_t)2 * n * 8, hipMemcpyDefault));
-    void* bufs[] = {dcol, dP, dN, duv};
-    for (void* b : bufs)
-        if (b) (void)hipFree(b);
     return SRT_OK;
 }
 
@@ -3444,15 +3491,16 @@ int srt_texture_lookup(srt_ctx* c, const srt_texture* tex, const uint8_t* texels
         return fail(SRT_ERR_ARG, "texture record outside the texel array");
     if (n <= 0) return SRT_OK;
     HIP_TRY(hipSetDevice(c->device));
+    CallBufs bufs;
     uint8_t* dtexels;
     srt_texture* dtex;
     double *duv, *drgb;
     uint32_t* dflags;
-    HIP_TRY(dalloc(&dtexels, texel_bytes));
-    HIP_TRY(dalloc(&dtex, 1));
-    HIP_TRY(dalloc(&duv, 2 * n));
-    HIP_TRY(dalloc(&drgb, 3 * n));
-    HIP_TRY(dalloc(&dflags, 1));
+    HIP_TRY(bufs.alloc(&dtexels, texel_bytes));
+    HIP_TRY(bufs.alloc(&dtex, 1));
+    HIP_TRY(bufs.alloc(&duv, 2 * n));
+    HIP_TRY(bufs.alloc(&drgb, 3 * n));
+    HIP_TRY(bufs.alloc(&dflags, 1));
     HIP_TRY(hipMemcpy(dtexels, texels, (size_t)texel_bytes, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dtex, tex, sizeof(srt_texture), hipMemcpyDefault));
     HIP_TRY(hipMemcpy(duv, uv, (size_t)2 * n * 8, hipMemcpyDefault));
@@ -3468,8 +3516,6 @@ int srt_texture_lookup(srt_ctx* c, const srt_texture* tex, const uint8_t* texels
     uint32_t flags = 0;
     HIP_TRY(hipMemcpy(&flags, dflags, 4, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(rgb, drgb, (size_t)3 * n * 8, hipMemcpyDefault));
-    void* bufs[] = {dtexels, dtex, duv, drgb, dflags};
-    for (void* b : bufs) (void)hipFree(b);
     return check_flags(flags);
 }
 
@@ -3487,6 +3533,7 @@ int srt_material_normal(srt_ctx* c, const srt_collider* col, const srt_texture* 
     }
     if (n <= 0) return SRT_OK;
     HIP_TRY(hipSetDevice(c->device));
+    CallBufs bufs;
     srt_material mrec{};
     mrec.type = SRT_GLOSSY;
     mrec.tex = mrec.tex_aux0 = mrec.tex_aux1 = -1;
@@ -3497,12 +3544,12 @@ int srt_material_normal(srt_ctx* c, const srt_collider* col, const srt_texture* 
     uint8_t* dtexels = nullptr;
     double *dP, *dor, *dN;
     uint32_t* dflags;
-    HIP_TRY(dalloc(&dcol, 1));
-    HIP_TRY(dalloc(&dmat, 1));
-    HIP_TRY(dalloc(&dP, 3 * n));
-    HIP_TRY(dalloc(&dor, n));
-    HIP_TRY(dalloc(&dN, 3 * n));
-    HIP_TRY(dalloc(&dflags, 1));
+    HIP_TRY(bufs.alloc(&dcol, 1));
+    HIP_TRY(bufs.alloc(&dmat, 1));
+    HIP_TRY(bufs.alloc(&dP, 3 * n));
+    HIP_TRY(bufs.alloc(&dor, n));
+    HIP_TRY(bufs.alloc(&dN, 3 * n));
+    HIP_TRY(bufs.alloc(&dflags, 1));
     HIP_TRY(hipMemcpy(dcol, col, sizeof(srt_collider), hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dmat, &mrec, sizeof(srt_material), hipMemcpyDefault));
     HIP_TRY(hipMemcpy(dP, P, (size_t)3 * n * 8, hipMemcpyDefault));
@@ -3510,8 +3557,8 @@ int srt_material_normal(srt_ctx* c, const srt_collider* col, const srt_texture* 
     HIP_TRY(hipMemset(dflags, 0, 4));
     SceneView S{};
     if (normalmap) {
-        HIP_TRY(dalloc(&dtex, 1));
-        HIP_TRY(dalloc(&dtexels, texel_bytes));
+        HIP_TRY(bufs.alloc(&dtex, 1));
+        HIP_TRY(bufs.alloc(&dtexels, texel_bytes));
         HIP_TRY(hipMemcpy(dtex, normalmap, sizeof(srt_texture), hipMemcpyDefault));
         HIP_TRY(hipMemcpy(dtexels, texels, (size_t)texel_bytes, hipMemcpyDefault));
         S.tex = (const RT_RO srt_texture*)dtex;
@@ -3525,22 +3572,20 @@ int srt_material_normal(srt_ctx* c, const srt_collider* col, const srt_texture* 
     uint32_t flags = 0;
     HIP_TRY(hipMemcpy(&flags, dflags, 4, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(N, dN, (size_t)3 * n * 8, hipMemcpyDefault));
-    void* bufs[] = {dcol, dmat, dP, dor, dN, dflags, dtex, dtexels};
-    for (void* b : bufs)
-        if (b) (void)hipFree(b);
     return check_flags(flags);
 }
 
 int srt_primary_rays(srt_ctx* c, const srt_camera* cam, const double* J, double* O, double* D) {
     if (!c || !cam || !J || !O || !D) return fail(SRT_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
+    CallBufs bufs;
     const int64_t n = (int64_t)cam->width * cam->height;
     double *dJ, *dO, *dD, *xs, *ys;
-    HIP_TRY(dalloc(&dJ, 4 * n));
-    HIP_TRY(dalloc(&dO, 3 * n));
-    HIP_TRY(dalloc(&dD, 3 * n));
-    HIP_TRY(dalloc(&xs, cam->width));
-    HIP_TRY(dalloc(&ys, cam->height));
+    HIP_TRY(bufs.alloc(&dJ, 4 * n));
+    HIP_TRY(bufs.alloc(&dO, 3 * n));
+    HIP_TRY(bufs.alloc(&dD, 3 * n));
+    HIP_TRY(bufs.alloc(&xs, cam->width));
+    HIP_TRY(bufs.alloc(&ys, cam->height));
     HIP_TRY(hipMemcpy(dJ, J, (size_t)4 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(xs, cam->xs, (size_t)cam->width * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(ys, cam->ys, (size_t)cam->height * 8, hipMemcpyDefault));
@@ -3552,8 +3597,6 @@ int srt_primary_rays(srt_ctx* c, const srt_camera* cam, const double* J, double*
     HIP_TRY(hipStreamSynchronize(c->f->stream));
     HIP_TRY(hipMemcpy(O, dO, (size_t)3 * n * 8, hipMemcpyDefault));
     HIP_TRY(hipMemcpy(D, dD, (size_t)3 * n * 8, hipMemcpyDefault));
-    void* bufs[] = {dJ, dO, dD, xs, ys};
-    for (void* p : bufs) (void)hipFree(p);
     return SRT_OK;
 }
 
@@ -3601,7 +3644,7 @@ int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n
     hipStream_t st = c->f->stream;
     HIP_TRY(hipMemcpyAsync(mt_key0(c), key, rtmt::N * 4, hipMemcpyHostToDevice, st));
     int final_pos = 0;
-    if ((rc = mt_win_ensure(&c->f->mt_win, c->f->mt_win_cap, (int64_t)rtmt::SEGS * rtmt::N))) return rc;
+    if ((rc = mt_win_ensure(c, *c->f, (int64_t)rtmt::SEGS * rtmt::N))) return rc;
     if ((rc = mt_launch(c, st, c->f->mt_win, mt_key0(c), pos, n_out, n_skip, dst, &final_pos))) return rc;
     if (host_out) HIP_TRY(hipMemcpyAsync(out, dst, (size_t)n_out * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(key_out, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost, st));
@@ -3676,7 +3719,10 @@ int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_ren
             return fail(SRT_ERR_ARG, "contexts must be the ranks 0..n-1 of one srt_comm_init_all group");
     if (a->jitter) return fail(SRT_ERR_ARG, "a group frame draws its jitter on the devices (mt or Philox)");
     if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
-    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_RGB_ROWS)) return fail(SRT_ERR_ARG, "group flags: ASYNC, RGB_ROWS");
+    if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_RGB_ROWS | SRT_RENDER_RGB_LOCAL))
+        return fail(SRT_ERR_ARG, "group flags: ASYNC, RGB_ROWS, RGB_LOCAL");
+    if ((a->flags & SRT_RENDER_RGB_LOCAL) && (a->out_rgb || (a->flags & SRT_RENDER_RGB_ROWS)))
+        return fail(SRT_ERR_ARG, "SRT_RENDER_RGB_LOCAL needs out_rgb NULL and no SRT_RENDER_RGB_ROWS");
     if (a->flags & SRT_RENDER_ASYNC) return render_group_async(ctxs, n, cam, a);
     // A frame whose passes overflowed a queue/ring, met a chain-mode tie or left the fixed-point range
     // is rendered again on every context (the gather pairs the ranks' tiles), from the same numpy
@@ -3703,7 +3749,7 @@ static int render_group_once(srt_ctx** ctxs, int n, const srt_camera* cam, const
     const bool want_rgb = a->out_rgb != nullptr;
     int rc = SRT_OK;
     srt_render_args aq = *a;
-    aq.flags = SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | (want_rgb ? SRT_RENDER_GATHER_RGB : 0);
+    aq.flags = SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | (want_rgb ? SRT_RENDER_GATHER_RGB : (a->flags & SRT_RENDER_RGB_LOCAL));
     aq.out_rgb = nullptr;  // rank 0 assembles into its slot buffers; copied to the caller's below
     aq.out_srgb8 = nullptr;
     for (int q = 0; q < n && !rc; ++q) {
@@ -3758,7 +3804,8 @@ static int render_group_once(srt_ctx** ctxs, int n, const srt_camera* cam, const
 static int render_group_async(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_render_args* a) {
     srt_render_args aq = *a;
     const bool rows = (a->flags & SRT_RENDER_RGB_ROWS) != 0;
-    aq.flags = SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | (rows ? SRT_RENDER_RGB_ROWS : (a->out_rgb ? SRT_RENDER_GATHER_RGB : 0));
+    aq.flags = SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | (a->flags & SRT_RENDER_RGB_LOCAL) |
+               (rows ? SRT_RENDER_RGB_ROWS : (a->out_rgb ? SRT_RENDER_GATHER_RGB : 0));
     int rc = SRT_OK;
     int queued = 0;
     for (int q = 0; q < n && !rc; ++q) {

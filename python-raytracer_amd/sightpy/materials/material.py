@@ -26,9 +26,13 @@ class Material:
         self.repeat = repeat
 
     def get_Normal(self, hit):
-        """Shading normal (material.py:18-36) at hit.point on the device (srt_material_normal): the
-        collider's normal, or the normal map's texel at the primitive's uv through the collider's
-        inverse_basis_matrix, normalised; times the hit orientation."""
+        """Shading normal (material.py:18-36) at hit.point: without a normal map the collider's
+        normal times the hit orientation, as the reference composes it (the collider's get_Normal is
+        its own device entry point); with one, on the device (srt_material_normal): the normal map's
+        texel at the primitive's uv through the collider's inverse_basis_matrix, normalised, times
+        the hit orientation."""
+        if self.normalmap is None:
+            return hit.collider.get_Normal(hit) * hit.orientation
         from .._backend import material_normal
         from ..utils.vector3 import vec3
 

@@ -68,8 +68,10 @@ class Scene:
         independent jitter on the GPU (Philox keyed by pixel and sample).  `batch_size` bounds the
         samples per device pass.
 
-        With several GPUs ($SIGHTPY_DEVICES, e.g. "0,1,2,3" or "all") the frame is split into
-        8-row bands dealt round-robin over the GPUs and gathered over RCCL (the reference's
+        With several GPUs ($SIGHTPY_DEVICES, e.g. "0,1,2,3" or "all") the frame is split into row
+        bands dealt round-robin over the GPUs (at most 8 bands per GPU: e.g. 27-row bands at 1080p
+        on 8 GPUs, 2-row bands for a Diffuse fan-out scene; rt_device.h shard_band_height) and
+        gathered over RCCL (the reference's
         multiprocessing.Pool over samples, scene.py:80-116, is replaced); the image does not depend
         on the number of GPUs.
         """

@@ -191,6 +191,83 @@ def test_headline_configs_1080p_rgb_match_oracle(builder, depth, spp, seed):
     _close_u8(out.srgb8, O.srgb_u8(rgb, 1080, 1920))
 
 
+def test_headline_frame_through_the_bench_path_matches_oracle():
+    """The exact headline frame (BASELINE configs[1]: example1 1920x1080, depth 5, 6 spp) through the
+    bench's own path -- numpy's stream generated on the GPU from a seeded numpy state, pipelined
+    (SRT_RENDER_ASYNC) frames into pinned host buffers, the fused kernel's in-kernel resolve -- against
+    the oracle on the same numpy draws (reference scene.py:71-140, example1.py:73).  The second of two
+    pipelined frames is checked (its key window comes from the first frame's end jump): linear RGB
+    within a pure 1e-5 relative bound on every value (no absolute floor), uint8 within +-1 at < 0.1 %
+    of the pixels, primary hit ids exact (a synchronous re-render from the same numpy state with hit
+    ids requested, equal to the pipelined frame bit for bit), per-depth ray counts equal, and numpy's
+    state advanced past both frames' sizing draws (scene.py:81)."""
+    import ctypes
+    from sightpy import _native as N
+    from oracle_pool import render_linear_pool
+
+    B = _backend()
+    W, H, D, spp, npix = 1920, 1080, 5, 6, 1920 * 1080
+    sc = scenes.example1(W, H, D)
+    # the reference's draws: per frame 6 samples x (x, y, disk r, disk phi), then one sizing get_ray
+    np.random.seed(0)
+    state0 = np.random.get_state()
+    sc.camera.draw_jitter(spp)
+    sc.camera.draw_jitter(1)
+    state1 = np.random.get_state()
+    jit2 = sc.camera.draw_jitter(spp)
+    sc.camera.draw_jitter(1)
+    state2 = np.random.get_state()
+
+    lib, ctx = B.context()
+    B.upload(sc)
+    cd = B.camera_desc(sc.camera)
+    N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))
+    outs = []
+    try:
+        for _ in range(2):
+            pu, pr = ctypes.c_void_p(), ctypes.c_void_p()
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * npix, ctypes.byref(pu)))
+            N.check(lib, lib.srt_host_alloc(ctx, 3 * npix * 8, ctypes.byref(pr)))
+            outs.append((pu, pr))
+        np.random.set_state(state0)
+        mt = N.MtState.from_numpy()
+        a = N.RenderArgs()
+        a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, H, 0
+        a.rows, a.jitter, a.out_hit_id = None, None, None
+        a.mt = ctypes.pointer(mt)
+        a.seed = 12345
+        a.flags = N.RENDER_ASYNC
+        for pu, pr in outs:
+            a.out_srgb8, a.out_rgb = pu, pr
+            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+        st = N.Stats()
+        N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(st)))
+        st = st.as_dict()
+        assert st["kernel_path"] == "fused"
+        mt.to_numpy()
+        got = np.random.get_state()
+        assert got[2] == state2[2] and np.array_equal(got[1], state2[1])
+        u8 = np.ctypeslib.as_array(ctypes.cast(outs[1][0], ctypes.POINTER(ctypes.c_uint8)), (H, W, 3)).copy()
+        rgb = np.ctypeslib.as_array(ctypes.cast(outs[1][1], ctypes.POINTER(ctypes.c_double)), (3, npix)).copy()
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"pipeline", 0))
+        for pu, pr in outs:
+            lib.srt_host_free(ctx, pu)
+            lib.srt_host_free(ctx, pr)
+    # the same frame again, synchronously, with the primary hit ids
+    np.random.set_state(state1)
+    again = B.render_scene(sc, spp, seed=12345, mt=True, want_hits=True)
+    assert np.array_equal(again.rgb, rgb) and np.array_equal(again.srgb8, u8)
+    ref, ids, counts = render_linear_pool("example1", W, H, D, jit2)
+    assert np.array_equal(again.hit_ids, ids)
+    assert st["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
+    nz = ref != 0.0
+    assert np.all(rgb[~nz] == 0.0)
+    rel = np.abs(rgb[nz] - ref[nz]) / np.abs(ref[nz])
+    assert rel.max() <= RTOL, rel.max()
+    _close_u8(u8, O.srgb_u8(ref, H, W))
+
+
 def test_example1_1080p_d5_ray_counts_match_reference_survey():
     # SURVEY.md section 6: seed 0, 6 spp -> rays per depth measured with the reference
     sc = scenes.example1(1920, 1080, 5)
