@@ -638,8 +638,16 @@ __device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3]
 // is traced in the thread too (no ray queues), and a single-pass frame resolves the pixel here
 // (P.fuse_resolve: average, sRGB, uint8; no framebuffer at all).  Otherwise the children are appended
 // to the depth-1 queue for k_trace.
+// (experiments) RT_PRIMARY_VGPR_CAP = k: k_primary allocates at most 2k VGPRs (amdgpu_num_vgpr counts
+// half the unified VGPR+AGPR file on gfx950), e.g. 80 -> 160: 3 waves/SIMD leave 32 registers per SIMD
+// free, room for one small wave of another kernel (the numpy-stream generator) beside them
+#ifdef RT_PRIMARY_VGPR_CAP
+#define RT_PRIMARY_ATTR __attribute__((amdgpu_num_vgpr(RT_PRIMARY_VGPR_CAP)))
+#else
+#define RT_PRIMARY_ATTR
+#endif
 template <uint32_t MATS, int OCC = 2, bool FUSE = false>
-__global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
+__global__ __launch_bounds__(BLOCK, OCC) RT_PRIMARY_ATTR void k_primary(TraceParams P0) {
     const TraceParams& P = P0;  // (read in place from the kernel arguments)
     stage_luts(P);
     const uint32_t shard = blockIdx.x % NSHARD;
@@ -1524,7 +1532,7 @@ struct srt_ctx {
     // band mode (a shard's rows of the numpy stream, rt_mt_kernel.h MtArgs::bands): per pass shape,
     // the segment list and its jump polynomials (host-made once, kept for the context's life)
     struct MtBandTab {
-        int64_t key[5];
+        int64_t key[6];
         uint64_t rows_hash;
         int nseg;
         int64_t band_len, band_period;  // merged segments store k % band_period < band_len (doubles)
@@ -1534,6 +1542,12 @@ struct srt_ctx {
     std::deque<MtBandTab> mt_bandtabs;  // (stable addresses: frames hold pointers into it)
     std::vector<std::pair<int64_t, uint32_t*>> mt_end_polys;  // frame-end jump polynomial per word count
     bool mt_bands_on = true;  // option "mt_bands"
+    // option "mt_short": doubles per segment of a whole frame's stream when nothing else is in flight
+    // (a synchronous frame -- Scene.render -- or the first of a pipeline): its generation cannot hide
+    // behind earlier frames, and a segment's serial generator (624-word blocks, ~0.5 us each) sets the
+    // frame's latency: 2^19-word tabulated segments 0.42 ms, 2^17-word ones ~0.1 ms for 4x the jumps,
+    // made in band mode (host jump polynomials, cached per frame shape); 0: tabulated segments
+    int64_t mt_short = 65536;
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
@@ -1871,6 +1885,7 @@ int mt_end_reset(srt_ctx* c) {
 // profiles/r04_jump_parts_ab.txt)
 int mt_jump_parts(const srt_ctx* c) { return c->mt_parts_opt ? c->mt_parts_opt : 4; }
 
+
 // The y words of `key` for a generation on `st`: those an end block made with the key (a final
 // window), else k_mt_y into the scratch buffer (one workgroup, ~34 blocks).  Generations of
 // different frames are ordered by the key they hand on, so one scratch buffer suffices.
@@ -1899,14 +1914,15 @@ int mt_end_poly_for(srt_ctx* c, int64_t n_words, const uint32_t** out) {
 // Regular runs (a shard's 8-row bands: equal length, equal spacing) with short gaps are merged while
 // a segment spans at most MT_MERGE_DOUBLES: it then generates through the other ranks' rows between
 // them (stores masked by band_len / band_period), trading one jump (~110 us of a CU) for a few
-// hundred generated blocks (a CU fraction); other runs are split at 2^18 doubles.
+// hundred generated blocks (a CU fraction); other runs are split at `split` doubles (2^18 for a
+// shard's rows, srt_ctx::mt_short for a whole frame generated with nothing else in flight).
 constexpr int MT_MAX_BANDS = 2048;
 constexpr int64_t MT_MERGE_DOUBLES = 150000;
 int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, const int32_t* rows, int n_rows,
-                  const srt_ctx::MtBandTab** out) {
+                  int64_t split, const srt_ctx::MtBandTab** out) {
     uint64_t h = 1469598103934665603ull;
     for (int k = 0; k < n_rows; ++k) h = (h ^ (uint64_t)(uint32_t)rows[k]) * 1099511628211ull;
-    const int64_t key[5] = {W, Hf, ns, plane_mask, n_rows};
+    const int64_t key[6] = {W, Hf, ns, plane_mask, n_rows, split};
     for (auto& t : c->mt_bandtabs)
         if (!memcmp(t.key, key, sizeof key) && t.rows_hash == h) { *out = &t; return SRT_OK; }
     // runs of consecutive rows (first row, count)
@@ -1948,7 +1964,7 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
                 } else {
                     int64_t n = (int64_t)runs[k].second * W;
                     while (n > 0) {
-                        const int64_t m = std::min<int64_t>(n, (int64_t)1 << 18);
+                        const int64_t m = std::min<int64_t>(n, split);
                         segs.insert(segs.end(), {d0, m, 0, l0});
                         d0 += m;
                         l0 += m;
@@ -1962,7 +1978,8 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
     *out = nullptr;
     if (nseg > MT_MAX_BANDS || nseg == 0) return SRT_OK;  // (the tabulated segments instead)
     std::vector<uint32_t> polys((size_t)nseg * rtmt::N, 0u);
-    const int nth = std::max(1, std::min<int>(8, (int)std::thread::hardware_concurrency()));
+    // (xpow_mod ~2.5 ms per polynomial: up to 16 host threads, the GPU boxes' CPU share per GPU)
+    const int nth = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
     for (int w = 0; w < nth; ++w)
         th.emplace_back([&, w] {
@@ -2399,6 +2416,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_short")) {
+        if (value != 0 && (value < 4096 || value > ((int64_t)1 << 24))) return fail(SRT_ERR_ARG, "mt_short: 0 or 4096 .. 2^24 doubles");
+        c->mt_short = value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "texel_rgbx")) { c->texel_rgbx = value != 0; return SRT_OK; }  // (next srt_upload_scene)
     if (!strcmp(key, "sky_prefetch")) { c->sky_prefetch = value != 0; return SRT_OK; }  // (next srt_upload_scene)
     if (!strcmp(key, "mt_jump_parts")) {
@@ -2796,10 +2818,16 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         for (auto& e : c->mt_end_polys) (void)hipFree(e.second);
         c->mt_end_polys.clear();
     }
-    if (use_mt && c->mt_bands_on && n_rows < Hf) {
+    // a whole frame with nothing in flight (synchronous, or the first of a pipeline): short segments in
+    // band mode (srt_ctx::mt_short); later pipelined frames generate behind their predecessors
+    // (tabulated 2^19-word segments, fewer jumps)
+    const bool mt_short = use_mt && c->mt_bands_on && c->mt_short > 0 && n_rows == Hf && c->async_pending == 0;
+    if (use_mt && c->mt_bands_on && (n_rows < Hf || mt_short)) {
         const int last_ns = a->spp - (F.npass - 1) * batch;
+        const int64_t split = n_rows < Hf ? (int64_t)1 << 18 : c->mt_short;
         for (int k = 0; k < 2; ++k) {
-            if ((rc = mt_band_table(c, W, Hf, k == 0 ? batch : last_ns, mt_pm, rows_src, n_rows, &mt_bt[k]))) return rc;
+            if ((rc = mt_band_table(c, W, Hf, k == 0 ? batch : last_ns, mt_pm, rows_src, n_rows, split, &mt_bt[k])))
+                return rc;
             if (mt_bt[k]) mt_win_need = std::max(mt_win_need, (int64_t)(mt_bt[k]->nseg + 1) * rtmt::N);
         }
         if (!mt_bt[0] || !mt_bt[1]) mt_bt[0] = mt_bt[1] = nullptr;
@@ -3926,6 +3954,27 @@ int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
     return SRT_OK;
 }
 #endif
+
+int srt_debug_mt_residue(srt_ctx* c, int64_t* nonzero_words) {
+    if (!c || !nonzero_words) return fail(SRT_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = finish_async(c, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    int64_t nz = 0;
+    std::vector<uint32_t> h;
+    auto count = [&](const uint32_t* d, int64_t words) -> int {
+        h.resize((size_t)words);
+        HIP_TRY(hipMemcpy(h.data(), d, (size_t)words * 4, hipMemcpyDeviceToHost));
+        for (uint32_t w : h) nz += w != 0u;
+        return SRT_OK;
+    };
+    for (FrameSlot& f : c->slots)
+        if (f.mt_win && (rc = count(f.mt_win, f.mt_win_cap))) return rc;
+    if (c->mt && (rc = count(mt_end_acc(c), rtmt::N + 1))) return rc;
+    *nonzero_words = nz;
+    return SRT_OK;
+}
 
 int srt_synchronize(srt_ctx* c) {
     if (!c) return fail(SRT_ERR_ARG, "null ctx");

@@ -100,8 +100,14 @@ constexpr size_t MT_LDS_BYTES = (size_t)mt_jump_lds_words(MT_MIN_PARTS) * 4;  //
 inline size_t mt_jump_lds_bytes(int parts) { return (size_t)mt_jump_lds_words(parts) * 4; }
 // generator threads per segment: 5 waves (227 make the next block, 312 store the current one).
 // Measured (222 segments, ex1 1080p pinhole planes): 1 wave 1.17 ms, 4 waves 0.64, 5 waves 0.50,
-// 8 waves 0.50 -- one wave is VALU-issue bound (~3000 cycles per 624-word block)
+// 8 waves 0.50 -- one wave is VALU-issue bound (~3000 cycles per 624-word block).  Round 5, with the
+// one-range store test per block: one wave 281 us against 131 us per synchronous ex1 frame (2^17-word
+// segments), and pipelined frames 1.60 against 0.99 ms (profiles/r05_mt_generator_ab.txt)
+#ifdef MT_GEN_THREADS_OVERRIDE  // (experiments)
+constexpr int MT_GEN_THREADS = MT_GEN_THREADS_OVERRIDE;
+#else
 constexpr int MT_GEN_THREADS = 320;
+#endif
 
 // workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic, not for its global
 // stores (__syncthreads() would also drain the output stores)
@@ -390,20 +396,42 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, uint32_t* win) {
             kb += A.plane;
         }
         const uint32_t* cur = p;
+        // the block's pairs k in [klo, khi) are all stored when no merged-band mask applies and the
+        // (at most two) planes they lie in are stored planes: one range test per pair (the usual
+        // block); otherwise every pair's plane and band are tested
+        const int klo = max(kq, 0), khi = min(kq + 312, g.kend);
+        bool every = !g.masked;
+        if (every && A.plane > 0)
+            every = (klo >= kb || ((A.plane_mask >> (int)(pidx & 3)) & 1)) &&
+                    (khi <= kb || ((A.plane_mask >> (int)((pidx + 1) & 3)) & 1));
+        if (every) {
 #pragma unroll
-        for (int i = 0; i < (312 + NT - 1) / NT; ++i) {
-            const int t = lane + NT * i;
-            const int k = kq + t;
-            if (t < 312 && k >= 0 && k < g.kend &&
-                (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1)) &&
-                (!g.masked || (uint32_t)k % (uint32_t)A.band_period < (uint32_t)A.band_len)) {
-                const int o = off0 + 2 * (c0 + t);  // in-block offset of the pair's first word: -1 .. 622
-                const uint32_t x0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
-                const uint32_t x1 = cur[o + 1];
-                const int64_t ko = cm ? (int64_t)((uint32_t)k / (uint32_t)A.band_period) * A.band_len +
-                                            (uint32_t)k % (uint32_t)A.band_period
-                                      : (int64_t)k;
-                outp[ko] = rtmt::to_double(rtmt::temper(x0), rtmt::temper(x1));
+            for (int i = 0; i < (312 + NT - 1) / NT; ++i) {
+                const int t = lane + NT * i;
+                const int k = kq + t;
+                if (t < 312 && k >= klo && k < khi) {
+                    const int o = off0 + 2 * (c0 + t);  // in-block offset of the pair's first word: -1 .. 622
+                    const uint32_t x0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
+                    const uint32_t x1 = cur[o + 1];
+                    outp[k] = rtmt::to_double(rtmt::temper(x0), rtmt::temper(x1));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < (312 + NT - 1) / NT; ++i) {
+                const int t = lane + NT * i;
+                const int k = kq + t;
+                if (t < 312 && k >= 0 && k < g.kend &&
+                    (A.plane == 0 || ((A.plane_mask >> (int)((k < kb ? pidx : pidx + 1) & 3)) & 1)) &&
+                    (!g.masked || (uint32_t)k % (uint32_t)A.band_period < (uint32_t)A.band_len)) {
+                    const int o = off0 + 2 * (c0 + t);
+                    const uint32_t x0 = o >= 0 ? cur[o] : ring[prev * rtmt::N + rtmt::N - 1];
+                    const uint32_t x1 = cur[o + 1];
+                    const int64_t ko = cm ? (int64_t)((uint32_t)k / (uint32_t)A.band_period) * A.band_len +
+                                                (uint32_t)k % (uint32_t)A.band_period
+                                          : (int64_t)k;
+                    outp[ko] = rtmt::to_double(rtmt::temper(x0), rtmt::temper(x1));
+                }
             }
         }
         if (g.chain || g.dump) {
@@ -418,10 +446,9 @@ __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, uint32_t* win) {
         prev = slot;
         slot = next;
         next = next == 2 ? 0 : next + 1;
-        if (NT == 64)
-            __syncthreads();  // one wave: orders the block's LDS writes before the next block's reads
-        else
-            mt_barrier();
+        // (one wave: its LDS operations complete in order, the barrier is nearly free; the output
+        // stores are not waited for)
+        mt_barrier();
     }
 }
 

@@ -13,7 +13,7 @@ from . import _native as N
 from ._lower import lower_scene, camera_desc, collider_record
 from .utils.vector3 import vec3
 
-_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": {}, "buffers": {}, "group": None}
+_STATE = {"lib": None, "ctx": None, "device": None, "scene_sig": {}, "buffers": {}, "pinned": {}, "group": None}
 
 
 class RenderResult:
@@ -37,6 +37,12 @@ def _env_options(lib, ctx):
         N.check(lib, lib.srt_set_option(ctx, b"frame_kernel", int(os.environ["SIGHTPY_FRAME_KERNEL"])))
     if os.environ.get("SIGHTPY_DETERMINISTIC") is not None:  # 0: f64 atomics instead of fixed-point sums
         N.check(lib, lib.srt_set_option(ctx, b"deterministic", int(os.environ["SIGHTPY_DETERMINISTIC"])))
+    # any library option: SIGHTPY_OPTIONS="key=value,key=value" (srt_set_option; e.g. A/B runs of the
+    # whole test suite on another generator or kernel strategy)
+    for kv in os.environ.get("SIGHTPY_OPTIONS", "").split(","):
+        if kv.strip():
+            k, v = kv.split("=")
+            N.check(lib, lib.srt_set_option(ctx, k.strip().encode(), int(v)))
 
 
 def _device_spec():
@@ -122,6 +128,23 @@ def upload(scene, extra_media=(), force=False, ctx=None):
     return L
 
 
+def pinned_buffer(name, nbytes):
+    """A named pinned host allocation of the context (srt_host_alloc), grown on demand and kept across
+    calls, as a uint8 numpy array: the device copies into it at full PCIe rate (a pageable destination
+    goes through the runtime's staging copies)."""
+    lib, ctx = context()
+    cur = _STATE["pinned"].get(name)
+    if cur is None or cur[1] < nbytes:
+        if cur is not None:
+            N.check(lib, lib.srt_host_free(ctx, cur[0]))
+            del _STATE["pinned"][name]
+        p = ctypes.c_void_p()
+        N.check(lib, lib.srt_host_alloc(ctx, max(int(nbytes), 8), ctypes.byref(p)))
+        cur = (p, int(nbytes))
+        _STATE["pinned"][name] = cur
+    return np.ctypeslib.as_array(ctypes.cast(cur[0], ctypes.POINTER(ctypes.c_uint8)), (cur[1],))[:nbytes]
+
+
 def device_buffer(name, nbytes):
     """A named device allocation of the context, grown on demand (kept across calls)."""
     lib, ctx = context()
@@ -183,11 +206,14 @@ def _default_seed():
 
 
 def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False,
-                 jitter_device=None, mt=False):
+                 jitter_device=None, mt=False, pinned_u8=False):
     """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG;
     `jitter_device`: the same uniforms already in device memory (numpy_uniforms); `mt=True`: the
     jitter is numpy's global stream generated on the device (the reference's draws, including the
-    sizing draw of scene.py:81), and numpy's global state is advanced past it."""
+    sizing draw of scene.py:81), and numpy's global state is advanced past it.  `pinned_u8`: the
+    uint8 image lands in the context's pinned host buffer (a view, valid until the next such call)
+    instead of a new array.  Without `want_rgb` the linear RGB is resolved and kept in HBM
+    (SRT_RENDER_RGB_LOCAL), as the reference keeps it internal."""
     lib, ctx = context()
     upload(scene)
     cam = scene.camera
@@ -218,11 +244,12 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
         state = N.MtState.from_numpy()
         a.mt = ctypes.pointer(state)
     rgb = np.empty((3, npix)) if want_rgb else None
-    u8 = np.empty((npix, 3), dtype=np.uint8)
+    u8 = (pinned_buffer("render_u8", 3 * npix) if pinned_u8 else np.empty(3 * npix, dtype=np.uint8)).reshape(npix, 3)
     hits = np.empty((spp, npix), dtype=np.int32) if want_hits else None
     a.out_rgb = N.ptr(rgb)
     a.out_srgb8 = N.ptr(u8)
     a.out_hit_id = N.ptr(hits)
+    a.flags = 0 if want_rgb else N.RENDER_RGB_LOCAL
     st = N.Stats()
     N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
     if state is not None:
@@ -250,6 +277,7 @@ def render_group(scene, spp, seed=None, batch_size=None, want_rgb=True, mt=True)
     rgb = np.empty((3, W * H)) if want_rgb else None
     u8 = np.empty((W * H, 3), dtype=np.uint8)
     a.out_rgb, a.out_srgb8 = N.ptr(rgb), N.ptr(u8)
+    a.flags = 0 if want_rgb else N.RENDER_RGB_LOCAL  # (every GPU keeps its rows of the linear RGB)
     st = N.Stats()
     N.check(lib, lib.srt_render_group(ctxs, len(ctxs), ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
     if state is not None:

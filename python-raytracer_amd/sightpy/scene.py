@@ -93,7 +93,7 @@ class Scene:
                 self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
             # only the uint8 image leaves the GPU (the linear RGB stays there: 8x fewer PCIe bytes)
             out = B.render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size,
-                                 want_rgb=False, mt=(rng == "numpy"))
+                                 want_rgb=False, mt=(rng == "numpy"), pinned_u8=True)
         self.last_stats = out.stats
         print("Render Took", time.time() - t0)
         return Image.fromarray(out.srgb8, "RGB")

@@ -156,3 +156,80 @@ def test_host_jump_polynomials():
 
         words = G.raw_words([int(v) for v in key], J + 624)
         assert np.array_equal(got[1:], np.array(words[J + 1:J + 624], dtype=np.uint32))
+
+
+def _mt_residue():
+    import ctypes
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    nz = ctypes.c_int64(-1)
+    N.check(lib, lib.srt_debug_mt_residue(ctx, ctypes.byref(nz)))
+    return nz.value
+
+
+@pytest.mark.gpu
+def test_generator_state_is_clean_between_frames_of_changing_shapes():
+    """Every generation leaves the segment-window tables, the end accumulator and its counter zero (the
+    next generation's jump parts XOR into them): synchronous whole frames (short segments, band mode),
+    pipelined frames (tabulated segments, frame-end jumps), a row shard (band mode), another frame
+    shape, and the tabulated segments for a synchronous frame (mt_short=0)."""
+    import ctypes
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    sc = scenes.example1(320, 240, 3)
+    np.random.seed(3)
+    B.render_scene(sc, 2, seed=1, mt=True)
+    assert _mt_residue() == 0
+    B.upload(sc)
+    cd = B.camera_desc(sc.camera)
+    mt = N.MtState.from_numpy()
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, 240, 0
+    a.rows, a.jitter, a.out_hit_id, a.seed = None, None, None, 1
+    a.mt = ctypes.pointer(mt)
+    a.flags = N.RENDER_ASYNC | N.RENDER_RGB_LOCAL
+    u8 = [B.device_buffer("residue_u8_%d" % k, 3 * 320 * 240) for k in range(4)]
+    for k in range(4):
+        a.out_srgb8, a.out_rgb = u8[k], None
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+    N.check(lib, lib.srt_render_finish(ctx, None))
+    mt.to_numpy()
+    assert _mt_residue() == 0
+    rows = np.arange(5, 240, 3)
+    B.render_scene(sc, 2, seed=1, mt=True, rows=rows)
+    assert _mt_residue() == 0
+    B.render_scene(scenes.example1(200, 150, 3), 3, seed=1, mt=True)
+    assert _mt_residue() == 0
+    N.check(lib, lib.srt_set_option(ctx, b"mt_short", 0))
+    try:
+        B.render_scene(sc, 2, seed=1, mt=True)
+        assert _mt_residue() == 0
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_short", 65536))
+
+
+@pytest.mark.gpu
+def test_short_segment_frames_equal_tabulated_segment_frames():
+    """A synchronous frame's numpy stream in short segments (band mode, option mt_short) and in the
+    tabulated 2^19-word segments: the same image and the same numpy state afterwards (1080p, the
+    headline's draw)."""
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    sc = scenes.example1(1920, 1080, 3)
+    np.random.seed(11)
+    a = B.render_scene(sc, 2, seed=1, mt=True)
+    sa = np.random.get_state()
+    N.check(lib, lib.srt_set_option(ctx, b"mt_short", 0))
+    try:
+        np.random.seed(11)
+        b = B.render_scene(sc, 2, seed=1, mt=True)
+        sb = np.random.get_state()
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_short", 65536))
+    assert np.array_equal(a.rgb, b.rgb) and np.array_equal(a.srgb8, b.srgb8)
+    assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])

@@ -26,9 +26,17 @@ def main():
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
     ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--profile", action="store_true", help="cProfile one render (host-side breakdown)")
+    ap.add_argument("--option", action="append", default=[], help="srt_set_option KEY=VALUE (repeatable)")
     a = ap.parse_args()
     builder, W, H, depth, spp, label = CONFIGS[a.config]
     sc = getattr(scenes, builder)(W, H, depth)
+    if a.option:
+        from sightpy import _backend as B, _native as N
+
+        lib, ctx = B.context()
+        for kv in a.option:
+            k, v = kv.split("=")
+            N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
     np.random.seed(0)
     sc.render(spp)  # warmup: scene upload, queue sizing
     times = []
@@ -50,6 +58,7 @@ def main():
     rays = sc.last_stats["total_rays"]
     best, med = min(times), float(np.median(times))
     print(json.dumps({"what": "Scene.render(%d) via the public API, host buffers (PCIe-inclusive)" % spp,
+                      "options": a.option,
                       "workload": label, "image": list(img.size), "rays_per_frame": int(rays),
                       "ms_median": round(med * 1e3, 3), "ms_min": round(best * 1e3, 3),
                       "Mrays_per_s_median": round(rays / med / 1e6, 1), "repeats": a.repeats}))
