@@ -527,6 +527,10 @@ def main():
                     help="with --shard-of: the rank rehearsed, or 'all' / 'all-reversed' (every rank in turn, "
                          "from rank 0 or from the last; ms_per_step = the slowest rank, value = all ranks' rays / "
                          "that time)")
+    ap.add_argument("--rehearse-assemble", action="store_true",
+                    help="with --shard-of N: rank 0's rehearsed frame also assembles the whole frame from its tile and N-1 "
+                         "stand-in tiles (k_assemble) and copies the whole uint8 frame to the host, as a sharded rank 0 "
+                         "does after the RCCL gather (library option rehearse_assemble)")
     ap.add_argument("--shard-bands", type=int, default=0,
                     help="most row bands per rank (library option shard_bands; default rt_device.h shard_kmax)")
     ap.add_argument("--shard-snake", type=int, default=-1,
@@ -606,6 +610,9 @@ def main():
                     for r in ranks}
         rows32 = rehearse[min(ranks)]
         npix_full = max(len(v) for v in rehearse.values()) * W  # the shards' outputs
+        if args.rehearse_assemble:
+            N.check(lib, lib.srt_set_option(ctx, b"rehearse_assemble", args.shard_of))
+            npix_full = W * H  # (rank 0 hands back the whole frame)
 
     # outputs: the whole frame in pinned host memory, one pair of buffers per frame in flight (N > 1:
     # the uint8 image on rank 0, gathered over RCCL; the linear RGB in the shared frames, every rank)

@@ -391,8 +391,9 @@ int srt_device_free(srt_ctx* ctx, void* ptr);
 int srt_memcpy(srt_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int srt_synchronize(srt_ctx* ctx);
 /* Diagnostic: waits for the context's frames and counts the nonzero words of the numpy-stream
- * generator's state that must be zero between generations (every frame slot's segment-window table,
- * the end-window accumulator and its arrival counter): 0 on a healthy context. */
+ * generator's state that must be zero between generations (every frame slot's segment windows -- the
+ * XOR targets of the jump parts, all but window 0, the key's copy --, the end-window accumulator and
+ * its arrival counter): 0 on a healthy context. */
 int srt_debug_mt_residue(srt_ctx* ctx, int64_t* nonzero_words);
 const char* srt_last_error(void);
 

@@ -16,6 +16,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <utility>
+
 #include "../../include/sightpy_rt.h"
 
 // Scene tables are read-only while a kernel runs.  In the device compilation they are addressed
@@ -87,6 +89,27 @@ constexpr uint32_t MAT_TRI = 0x80u;   // Triangle colliders intersected one by o
 constexpr uint32_t MAT_NMAP = 0x100u; // a normal-mapped material (shading_normal's texel path)
 constexpr uint32_t MAT_GENERIC = MAT_ALL | MAT_TRI | MAT_NMAP;
 constexpr uint32_t mat_bit(int type) { return 1u << type; }
+// Collider sequence known at compile time (bits 12..31 of a variant's feature mask, 0: the scene's
+// collider list read at run time): bits 0..3 of the sequence hold the count n (1..8), then 2 bits per
+// collider its type (SRT_SPHERE .. SRT_TRIANGLE), collider 0 first.  A kernel instantiated for a
+// sequence intersects the colliders in straight-line code (no loop, no type switch: the compiler
+// shares common subexpressions between colliders and interleaves their independent arithmetic); the
+// host runs it only on scenes whose colliders have exactly those types in that order.
+constexpr int SEQ_SHIFT = 12;
+constexpr int SEQ_MAX = 8;
+constexpr uint32_t seq_of(uint32_t feat) { return feat >> SEQ_SHIFT; }
+constexpr int seq_count(uint32_t q) { return (int)(q & 15u); }
+constexpr int seq_type(uint32_t q, int k) { return (int)((q >> (4 + 2 * k)) & 3u); }
+// the sequence code of n collider types (n <= SEQ_MAX), 0 if it cannot be encoded
+RT_HD uint32_t seq_encode(const int* types, int n) {
+    if (n < 1 || n > SEQ_MAX) return 0u;
+    uint32_t q = (uint32_t)n;
+    for (int k = 0; k < n; ++k) {
+        if (types[k] < 0 || types[k] > 3) return 0u;
+        q |= (uint32_t)types[k] << (4 + 2 * k);
+    }
+    return q;
+}
 
 struct d3 {
     double x, y, z;
@@ -675,8 +698,7 @@ RT_HD uint64_t bvh_entry(double tn, int32_t code) {
     return ((uint64_t)bvh_f2u(f) << 32) | (uint32_t)code;
 }
 RT_HD int32_t bvh_code(int32_t child, int32_t count) {
-    // (the negation in uint32_t: defined for every input, BVH_EMPTY included, though callers pass it
-    // only non-empty children)
+    // (the negation in uint32_t: defined for every input, BVH_EMPTY included)
     if (child >= 0) return child;
     const uint32_t leaf = (0u - (uint32_t)child) - 1u;
     return (int32_t)(0u - (1u + ((leaf << 6) | (uint32_t)count)));
@@ -688,7 +710,7 @@ RT_HD void bvh_children(const RT_RO BvhNode& nd, d3 O, d3 inv, double limit, boo
                         int32_t c[4]) {
 RT_UNROLL
     for (int k = 0; k < 4; ++k) {
-        c[k] = nd.child[k] == BVH_EMPTY ? BVH_EMPTY : bvh_code(nd.child[k], nd.count[k]);
+        c[k] = bvh_code(nd.child[k], nd.count[k]);  // (an empty slot's code is never used: t = INFINITY)
         double tn;
         const bool hit = nd.child[k] != BVH_EMPTY && box4_hit(nd, k, O, inv, tn) && (strict ? tn < limit : tn <= limit);
         t[k] = hit ? tn : INFINITY;
@@ -797,6 +819,37 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
 
 // BVH: compile the mesh traversal in (kernels instantiated for scenes without a BVH leave it out:
 // its stack would otherwise cost scratch and registers in every kernel)
+// One collider of the nearest-hit search of a collider sequence (its TYPE known at compile time),
+// merged into (best, id, bo, ties, nan) as nearest_hit's loop does
+template <uint32_t FEAT, int TYPE>
+RT_HD void nearest_step(const RT_RO srt_collider& cc, int c, d3 O, d3 D, double& best, int& id, double& bo,
+                        bool& ties, bool& nan) {
+    double o;
+    if (TYPE == SRT_CUBOID && cc.p[42] != 0.0 && id >= 0) {
+        // axis-aligned box around O (a SkyBox): leaving it takes t >= dmin / max|D_i|, dmin the
+        // distance from O to the nearest face, and its slab t's are NaN-free (no face passes
+        // through O).  Far beyond the nearest hit so far it can be neither nearest nor tied.
+        const RT_RO double* p = cc.p;
+        double dmin = np_min(np_min(np_min(O.x - p[12], p[15] - O.x), np_min(O.y - p[13], p[16] - O.y)),
+                             np_min(O.z - p[14], p[17] - O.z));
+        double dmax = np_max(np_max(fabs(D.x), fabs(D.y)), fabs(D.z));
+        if (dmin > 0.0 && best * dmax < 0.5 * dmin) return;
+    }
+    double t;
+    if constexpr (TYPE == SRT_SPHERE) t = sphere_hit(cc.p, O, D, o);
+    else if constexpr (TYPE == SRT_PLANE) t = plane_hit(cc.p, O, D, o);
+    else if constexpr (TYPE == SRT_CUBOID) t = cuboid_hit(cc.p, O, D, o);
+    else t = triangle_hit(cc.p, O, D, o);
+    if (t != t) nan = true;
+    if (t < best) { best = t; id = c; bo = o; ties = false; }
+    else if (t == best && id >= 0) ties = true;
+}
+template <uint32_t FEAT, int... K>
+RT_HD void nearest_seq(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties, bool& nan,
+                       std::integer_sequence<int, K...>) {
+    (nearest_step<FEAT, seq_type(seq_of(FEAT), K)>(S.col[K], K, O, D, best, id, bo, ties, nan), ...);
+}
+
 template <uint32_t FEAT = MAT_GENERIC | MAT_BVH>
 RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bool& ties) {
     constexpr bool BVH = (FEAT & MAT_BVH) != 0;
@@ -805,26 +858,29 @@ RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bo
     double bo = FARAWAY;
     ties = false;
     bool nan = false;
-    // without a BVH `lin` is the identity: the loop then indexes the collider table directly
-    const int nl = BVH ? S.nlin : S.ncol;
-    for (int li = 0; li < nl; ++li) {
-        const int c = BVH ? S.lin[li] : li;
-        double o;
-        const RT_RO srt_collider& cc = S.col[c];
-        if (cc.type == SRT_CUBOID && cc.p[42] != 0.0 && id >= 0) {
-            // axis-aligned box around O (a SkyBox): leaving it takes t >= dmin / max|D_i|, dmin the
-            // distance from O to the nearest face, and its slab t's are NaN-free (no face passes
-            // through O).  Far beyond the nearest hit so far it can be neither nearest nor tied.
-            const RT_RO double* p = cc.p;
-            double dmin = np_min(np_min(np_min(O.x - p[12], p[15] - O.x), np_min(O.y - p[13], p[16] - O.y)),
-                                 np_min(O.z - p[14], p[17] - O.z));
-            double dmax = np_max(np_max(fabs(D.x), fabs(D.y)), fabs(D.z));
-            if (dmin > 0.0 && best * dmax < 0.5 * dmin) continue;
+    if constexpr (seq_of(FEAT) != 0u && !BVH) {
+        // the scene's colliders in straight-line code, in index order (the same merge as the loop)
+        nearest_seq<FEAT>(S, O, D, best, id, bo, ties, nan, std::make_integer_sequence<int, seq_count(seq_of(FEAT))>{});
+    } else {
+        // without a BVH `lin` is the identity: the loop then indexes the collider table directly
+        const int nl = BVH ? S.nlin : S.ncol;
+        for (int li = 0; li < nl; ++li) {
+            const int c = BVH ? S.lin[li] : li;
+            double o;
+            const RT_RO srt_collider& cc = S.col[c];
+            if (cc.type == SRT_CUBOID && cc.p[42] != 0.0 && id >= 0) {
+                // axis-aligned box around O (a SkyBox): see nearest_step
+                const RT_RO double* p = cc.p;
+                double dmin = np_min(np_min(np_min(O.x - p[12], p[15] - O.x), np_min(O.y - p[13], p[16] - O.y)),
+                                     np_min(O.z - p[14], p[17] - O.z));
+                double dmax = np_max(np_max(fabs(D.x), fabs(D.y)), fabs(D.z));
+                if (dmin > 0.0 && best * dmax < 0.5 * dmin) continue;
+            }
+            double t = collider_hit<FEAT>(cc, O, D, o);
+            if (t != t) nan = true;
+            if (t < best) { best = t; id = c; bo = o; ties = false; }
+            else if (t == best && id >= 0) ties = true;
         }
-        double t = collider_hit<FEAT>(cc, O, D, o);
-        if (t != t) nan = true;
-        if (t < best) { best = t; id = c; bo = o; ties = false; }
-        else if (t == best && id >= 0) ties = true;
     }
     if (BVH && S.bvh_nodes > 0) bvh_nearest(S, O, D, best, id, bo, ties);
     if (nan || best == FARAWAY) { tn = nan ? NAN : FARAWAY; on = FARAWAY; ties = false; return -1; }
@@ -899,23 +955,46 @@ RT_HD Child mkchild(d3 o, d3 d, d3 w, uint32_t medium, uint32_t dfl, uint32_t sl
 // min over the shadowed colliders of the distance along the light direction (glossy.py:53-59)
 // `stop`: the caller only asks whether the result is >= stop (seelight), so the BVH pass may stop
 // at the first shadowing triangle closer than that
+// One collider of the shadow test (glossy.py:53-59) of a collider sequence, as shadow_nearest's loop
+template <uint32_t FEAT, int TYPE>
+RT_HD void shadow_step(const SceneView& S, const RT_RO srt_collider& cc, int c, int light, d3 O, d3 L, double& best,
+                       bool& first) {
+    if (!(cc.flags & SRT_CF_SHADOW)) return;
+    double o, t;
+    if constexpr (TYPE == SRT_CUBOID) t = cuboid_hit_local(cc.p, O, ld3(S.light_local + ((int64_t)light * S.ncol + c) * 3), o);
+    else if constexpr (TYPE == SRT_SPHERE) t = sphere_hit(cc.p, O, L, o);
+    else if constexpr (TYPE == SRT_PLANE) t = plane_hit(cc.p, O, L, o);
+    else t = triangle_hit(cc.p, O, L, o);
+    best = first ? t : np_min(best, t);
+    first = false;
+}
+template <uint32_t FEAT, int... K>
+RT_HD void shadow_seq(const SceneView& S, int light, d3 O, d3 L, double& best, bool& first,
+                      std::integer_sequence<int, K...>) {
+    (shadow_step<FEAT, seq_type(seq_of(FEAT), K)>(S, S.col[K], K, light, O, L, best, first), ...);
+}
+
 template <uint32_t FEAT = MAT_GENERIC | MAT_BVH>
 RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L, double stop) {
     constexpr bool BVH = (FEAT & MAT_BVH) != 0;
     double best = FARAWAY;
     bool first = true;
-    const int nl = BVH ? S.nlin : S.ncol;
-    for (int li = 0; li < nl; ++li) {
-        const int c = BVH ? S.lin[li] : li;
-        const RT_RO srt_collider& cc = S.col[c];
-        if (!(cc.flags & SRT_CF_SHADOW)) continue;
-        double o, t;
-        if (cc.type == SRT_CUBOID)
-            t = cuboid_hit_local(cc.p, O, ld3(S.light_local + ((int64_t)light * S.ncol + c) * 3), o);
-        else
-            t = collider_hit<FEAT>(cc, O, L, o);
-        best = first ? t : np_min(best, t);
-        first = false;
+    if constexpr (seq_of(FEAT) != 0u && !BVH) {
+        shadow_seq<FEAT>(S, light, O, L, best, first, std::make_integer_sequence<int, seq_count(seq_of(FEAT))>{});
+    } else {
+        const int nl = BVH ? S.nlin : S.ncol;
+        for (int li = 0; li < nl; ++li) {
+            const int c = BVH ? S.lin[li] : li;
+            const RT_RO srt_collider& cc = S.col[c];
+            if (!(cc.flags & SRT_CF_SHADOW)) continue;
+            double o, t;
+            if (cc.type == SRT_CUBOID)
+                t = cuboid_hit_local(cc.p, O, ld3(S.light_local + ((int64_t)light * S.ncol + c) * 3), o);
+            else
+                t = collider_hit<FEAT>(cc, O, L, o);
+            best = first ? t : np_min(best, t);
+            first = false;
+        }
     }
     if (BVH && S.bvh_nodes > 0 && best >= stop) best = np_min(best, bvh_shadow(S, O, L, stop));
     return best;

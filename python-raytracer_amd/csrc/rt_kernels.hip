@@ -1127,9 +1127,31 @@ const Variant VARIANTS[] = {
     {MAT_GENERIC | MAT_BVH, k_primary<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC>,
      k_frame<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC, true>},
 };
-const Variant& pick_variant(uint32_t mats) {
+// Variants for scenes of a given collider sequence (rt_device.h seq_of: the colliders intersected in
+// straight-line code); a scene runs one when its colliders have exactly these types in this order
+// and its materials are covered.
+#ifdef RT_SEQ_VARIANTS
+constexpr uint32_t seq_bits(std::initializer_list<int> t) {
+    uint32_t q = (uint32_t)t.size();
+    int k = 0;
+    for (int v : t) q |= (uint32_t)v << (4 + 2 * k++);
+    return q << SEQ_SHIFT;
+}
+// example1 / the headline: two spheres, a plane, the sky box
+constexpr uint32_t MATS_SEQ_SSPC = MATS_GLOSSY_SKY | seq_bits({SRT_SPHERE, SRT_SPHERE, SRT_PLANE, SRT_CUBOID});
+const Variant SEQ_VARIANTS[] = {
+    {MATS_SEQ_SSPC, k_primary<MATS_SEQ_SSPC, OCC>, k_trace<MATS_SEQ_SSPC, OCC>, k_frame<MATS_SEQ_SSPC, OCC>,
+     k_trace<MATS_SEQ_SSPC, OCC, true>, k_primary<MATS_SEQ_SSPC, RT_FUSE_OCC, true>},
+};
+#endif
+const Variant& pick_variant(uint32_t mats, uint32_t seq = 0) {
 #ifdef RT_OCC_VARIANTS
     if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
+#endif
+#ifdef RT_SEQ_VARIANTS
+    if (seq)
+        for (const Variant& v : SEQ_VARIANTS)
+            if (seq_of(v.mats) == seq && (v.mats & mats) == mats) return v;
 #endif
     for (const Variant& v : VARIANTS)
         if ((v.mats & mats) == mats) return v;
@@ -1433,6 +1455,7 @@ struct FrameSlot {
     bool copy_pending = false;       // `copied` guards rgb / u8 of this slot
     hipEvent_t jit_ready = nullptr;  // recorded on the MT stream after this slot's jitter is generated
     hipEvent_t jit_free = nullptr;   // recorded on `stream` after the last kernel that reads the jitter
+    hipEvent_t mt_jumped = nullptr;  // recorded on the MT stream after this slot's jump kernel
     bool jit_busy = false;           // `jit_free` guards the jitter buffer
     uint32_t* mt_win = nullptr;      // segment windows of this slot's numpy-stream generation
     int64_t mt_win_cap = 0;
@@ -1507,6 +1530,8 @@ struct srt_ctx {
     int has_diffuse = 0;
     int fanout = 1;
     uint32_t mats = 0;  // material types present (selects the kernel variant)
+    uint32_t seq = 0;   // the scene's collider sequence (rt_device.h seq_encode; 0: none, or option collider_seq 0)
+    bool seq_on = true;  // option "collider_seq": kernels specialised to the scene's collider sequence when built
     std::vector<void*> scene_bufs;
     // texel pool (outside scene_bufs: survives re-uploads with the same texel_key)
     uint8_t* texels = nullptr;
@@ -1580,6 +1605,11 @@ struct srt_ctx {
     // 0.20 / 0.33 / 0.21, profiles/r04_mt_stream_ab.txt); 0 the frame's stream; 1 a stream of its own;
     // 2 a high-priority one
     int use_mt_stream = -1;
+    // option "mt_gen_stream": with the generation on the MT stream (whole pipelined frames), 1 runs a
+    // frame's generators on the frame's own stream after its jump kernel (event): the MT stream then
+    // carries only the chain of jump kernels (each makes the next frame's key), and frame k+1's jumps
+    // do not wait behind frame k's generators; 0 keeps jumps and generators in one stream order
+    int mt_gen_stream = 1;
     bool use_copy_stream = false;
     // option "deterministic" (default 1): contributions added to a pixel by other threads go into
     // order-independent fixed-point sums (bit-reproducible frames); 0: f64 atomics
@@ -1621,6 +1651,12 @@ struct srt_ctx {
     // of 8 (1.3 rounds) is faster per depth, 0.29 vs 0.35 (profiles/r03_fused_ab.txt)
     int fuse_primary = -1;
     int pix_groups_opt = 0;     // option "pix_groups": k_primary's sample groups per pixel (power of two; 0 auto)
+    // option "rehearse_assemble" = n (diagnostic, one GPU): a frame rendering rank 0's rows of an
+    // n-rank job (rows given, not SRT_RENDER_SHARDED) also does rank 0's assembly -- k_assemble of its
+    // tile and n - 1 stand-in tiles of the other ranks' shapes into the whole frame -- and hands back
+    // the whole frame's uint8 image (host copy of W x H x 3 bytes), as a sharded rank 0 does after the
+    // RCCL gather (the transfers themselves are not rehearsed)
+    int rehearse_assemble = 0;
     double* red = nullptr;      // srt_comm_allreduce scratch
 };
 
@@ -2010,7 +2046,7 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
 // the final window (next key) and its y come from the jump kernel's end block.
 int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, int pos, int64_t n_words,
                     const srt_ctx::MtBandTab& T, double* out, int* final_pos, const uint32_t* end_poly,
-                    hipEvent_t key_ready) {
+                    hipEvent_t key_ready, hipStream_t gst = nullptr, hipEvent_t jumped = nullptr) {
     const int64_t abs_end = pos + n_words;
     const int64_t dump_abs = ((abs_end + rtmt::N - 1) / rtmt::N - 1) * rtmt::N;
     MtArgs A{};
@@ -2045,7 +2081,13 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     MtArgs G = A;
     G.dump_dst = nullptr;
     G.y_next = nullptr;
-    hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
+    if (gst && gst != st) {  // the generators on their own stream, after the windows they start from
+        HIP_TRY(hipEventRecord(jumped, st));
+        HIP_TRY(hipStreamWaitEvent(gst, jumped, 0));
+    } else {
+        gst = st;
+    }
+    hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, gst, G, win);
     HIP_TRY(hipGetLastError());
     c->mt_dirty = false;
     c->mt_y_valid[c->mt_cur ^ 1] = true;
@@ -2064,7 +2106,8 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
 // frame's generation may start then, beside this one's generators.
 int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, int pos, int64_t n_out, int64_t n_skip,
               double* out, int* final_pos, int64_t plane = 0, int plane_mask = 15, const uint32_t* end_poly = nullptr,
-              int64_t end_at = 0, hipEvent_t key_ready = nullptr) {
+              int64_t end_at = 0, hipEvent_t key_ready = nullptr, hipStream_t gst = nullptr,
+              hipEvent_t jumped = nullptr) {
     uint32_t* keys[2] = {c->mt + MT_NTAB, c->mt + MT_NTAB + rtmt::N};
     const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
     if (plan.rounds.size() != 1) end_poly = nullptr;
@@ -2112,7 +2155,15 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
         MtArgs G = A;
         G.y_next = nullptr;
         if (end) G.dump_dst = nullptr;  // (made by the jump kernel)
-        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
+        // the generators on their own stream when the jump kernel made the final window (a one-round
+        // generation with the frame-end jump): nothing after them on `st` reads what they write
+        hipStream_t g = st;
+        if (gst && gst != st && end && plan.rounds.size() == 1) {
+            HIP_TRY(hipEventRecord(jumped, st));
+            HIP_TRY(hipStreamWaitEvent(gst, jumped, 0));
+            g = gst;
+        }
+        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, g, G, win);
         HIP_TRY(hipGetLastError());
         c->mt_dirty = false;
     }
@@ -2195,6 +2246,7 @@ int ensure_slot(FrameSlot& f) {
     HIP_TRY(hipEventCreateWithFlags(&f.resolved, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f.copied, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f.jit_free, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&f.mt_jumped, hipEventDisableTiming));
     HIP_TRY(dalloc(&f.counts, SRT_MAX_DEPTHS * NSHARD));
     HIP_TRY(dalloc(&f.flags, 2));
     HIP_TRY(dalloc(&f.shadow, NSHARD));
@@ -2217,6 +2269,7 @@ void free_slot(FrameSlot& f) {
     (void)hipEventDestroy(f.resolved);
     (void)hipEventDestroy(f.copied);
     (void)hipEventDestroy(f.jit_free);
+    (void)hipEventDestroy(f.mt_jumped);
     (void)hipStreamDestroy(f.stream);
     f = FrameSlot{};
 }
@@ -2416,6 +2469,13 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_gen_stream")) { c->mt_gen_stream = value != 0; return SRT_OK; }
+    if (!strcmp(key, "collider_seq")) { c->seq_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "rehearse_assemble")) {
+        if (value != 0 && (value < 2 || value > MAX_RANKS)) return fail(SRT_ERR_ARG, "rehearse_assemble: 0 or 2 .. 64");
+        c->rehearse_assemble = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "mt_short")) {
         if (value != 0 && (value < 4096 || value > ((int64_t)1 << 24))) return fail(SRT_ERR_ARG, "mt_short: 0 or 4096 .. 2^24 doubles");
         c->mt_short = value;
@@ -2678,6 +2738,12 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     if (lin_tri) c->mats |= MAT_TRI;  // Triangle colliders outside the BVH
     for (int i = 0; i < d->n_materials; ++i)
         if (d->materials[i].normalmap >= 0) c->mats |= MAT_NMAP;
+    c->seq = 0;
+    if (S.bvh_nodes == 0 && d->n_colliders <= SEQ_MAX) {
+        int types[SEQ_MAX];
+        for (int i = 0; i < d->n_colliders; ++i) types[i] = d->colliders[i].type;
+        c->seq = seq_encode(types, d->n_colliders);
+    }
     c->chain_ok = true;
     c->hint_key[0] = -1;  // ray counts of another scene are no plan for this one
     c->has_scene = true;
@@ -2784,7 +2850,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     }
     // fused paths (single-child scenes): by default when the frame's threads (sample groups
     // included, pix_groups) fill two rounds of the resident threads
-    F.fuse = !F.frame && c->fanout == 1 && c->chain_ok && pick_variant(c->mats).fused &&
+    F.fuse = !F.frame && c->fanout == 1 && c->chain_ok && pick_variant(c->mats, c->seq_on ? c->seq : 0).fused &&
              (c->fuse_primary > 0 ||
               (c->fuse_primary < 0 && npix * pix_groups(c, npix, batch, true) >= fused_items(c)));
     if (!F.fuse && !F.frame && c->fanout == 1 && c->chain_ok && c->hint_key[0] == npix && c->hint_key[1] == a->spp &&
@@ -2841,6 +2907,18 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * (jit_compact ? npix : W * Hf)
                                        : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
     const int64_t maxpix = sharded ? shard_max_rows(Hf, c->nranks, band, c->shard_snake) * W : 0;  // the gather's tile
+    // rank 0's assembly rehearsed (srt_ctx::rehearse_assemble): these rows are rank 0's of an n-rank job
+    int reh_n = 0;
+    int64_t reh_band = 1, reh_maxpix = 0;
+    if (c->rehearse_assemble > 1 && !sharded && a->rows && a->out_srgb8 && ptr_kind(a->out_srgb8) != 1) {
+        const int n = c->rehearse_assemble;
+        reh_band = shard_band_height(Hf, n, shard_kmax(Hf, n, c->shard_bands, c->fanout), c->shard_snake);
+        const std::vector<int32_t> r0 = band_rows(Hf, n, 0, reh_band, c->shard_snake);
+        if ((int)r0.size() == n_rows && std::equal(r0.begin(), r0.end(), rows_src)) {
+            reh_n = n;
+            reh_maxpix = shard_max_rows(Hf, n, reh_band, c->shard_snake) * W;
+        }
+    }
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
     // for them (and reports their errors)
     if (async && c->async_pending > 0) {
@@ -2854,6 +2932,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                           F.frame == pp.frame && F.chain_from == pp.chain_from && F.fuse == pp.fuse && F.W == pp.W && F.H == pp.H &&
                           F.groups == pp.groups && (F.groups == 1 || (int64_t)F.groups * 3 * npix <= c->f->fbg_cap) &&
                           F.sharded == pp.sharded && F.gather_rgb == pp.gather_rgb && F.use_mt == pp.use_mt &&
+                          (!reh_n || (c->f->g_u8_cap >= reh_n * reh_maxpix * 3 && c->f->full_u8_cap >= 3 * W * Hf)) &&
                           (!sharded || c->rank != 0 ||
                            (c->f->g_u8_cap >= c->nranks * maxpix * 3 && c->f->full_u8_cap >= 3 * W * Hf &&
                             (!gather_rgb || (c->f->g_rgb_cap >= c->nranks * maxpix * 3 && c->f->full_rgb_cap >= 3 * W * Hf)))) &&
@@ -2892,6 +2971,13 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
         if (!r && use_mt) r = mt_win_ensure(c, *c->f, mt_win_need);
         if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
+        if (!r && reh_n) {
+            const int64_t had = c->f->g_u8_cap;
+            r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, reh_n * reh_maxpix * 3);
+            if (!r && c->f->g_u8_cap != had && hipMemset(c->f->g_u8, 0, (size_t)c->f->g_u8_cap) != hipSuccess)
+                r = fail(SRT_ERR_HIP, "hipMemset failed");  // (stand-in tiles: defined bytes)
+            if (!r) r = ensure_buf(&c->f->full_u8, c->f->full_u8_cap, 3 * W * Hf);
+        }
         if (!r && sharded && c->rank == 0) {
             r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, c->nranks * maxpix * 3);
             if (!r) r = ensure_buf(&c->f->full_u8, c->f->full_u8_cap, 3 * W * Hf);
@@ -2934,7 +3020,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         }
     }
     if (use_mt && !c->mt_done) HIP_TRY(hipEventCreateWithFlags(&c->mt_done, hipEventDisableTiming));
-    const Variant& V = pick_variant(c->mats);
+    const Variant& V = pick_variant(c->mats, c->seq_on ? c->seq : 0);
     // resolve targets: outputs in device memory are written in place by the resolve; host outputs
     // are resolved into the slot buffers and copied by DMA on the frame's stream (57 GB/s measured
     // for the ex1 1080p RGB, against 28 GB/s for a resolve kernel storing straight into pinned
@@ -3034,13 +3120,15 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 const uint32_t* end_poly = nullptr;
                 if (end && (rc = mt_end_poly_for(c, n_words, &end_poly))) return rc;
                 // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
+                // (a pipelined whole frame's generators on its own stream: see srt_ctx::mt_gen_stream)
+                hipStream_t gst = (mst != c->f->stream && c->mt_gen_stream && end) ? c->f->stream : mst;
                 if (band) {
                     if ((rc = mt_launch_bands(c, mst, c->f->mt_win, mt_key, mt_pos, n_words, *bt, c->f->jit, &mt_pos,
-                                              end_poly, p + 1 == F.npass ? c->mt_done : nullptr)))
+                                              end_poly, p + 1 == F.npass ? c->mt_done : nullptr, gst, c->f->mt_jumped)))
                         return rc;
                 } else if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos,
                                            W * Hf, mt_pm, end_poly, end ? (int64_t)rtmt::end_jump(n_words) : 0,
-                                           end ? c->mt_done : nullptr))) {
+                                           end ? c->mt_done : nullptr, gst, c->f->mt_jumped))) {
                     return rc;
                 }
                 // otherwise the next frame's stream may start as soon as this one's is generated
@@ -3210,6 +3298,20 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 G.host_rgb = (a->out_rgb && !rgb_dev && gather_rgb) ? a->out_rgb : nullptr;
             }
         }
+        const uint8_t* u8_src = c->f->u8;
+        int64_t u8_bytes = 3 * npix;
+        if (reh_n) {
+            GatherTiles T{};
+            for (int q = 0; q < reh_n; ++q) {
+                T.u8[q] = q == 0 ? c->f->u8 : c->f->g_u8 + (int64_t)q * reh_maxpix * 3;
+                T.npix[q] = shard_rank_rows(Hf, reh_n, q, reh_band, c->shard_snake) * W;
+            }
+            hipLaunchKernelGGL(k_assemble, dim3(grid_for(W * Hf, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, T, reh_n,
+                               reh_band, c->shard_snake, W, Hf, c->f->full_u8, (double*)nullptr);
+            HIP_TRY(hipGetLastError());
+            u8_src = c->f->full_u8;
+            u8_bytes = 3 * W * Hf;
+        }
         if (async) {
             // (a synchronous frame gathers after its retries: every rank gathers each frame once)
             if (sharded && !c->defer_gather && (rc = gather_frame(c))) return rc;
@@ -3222,7 +3324,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                     HIP_TRY(hipStreamWaitEvent(cs, c->f->resolved, 0));
                 }
                 if (a->out_srgb8 && !u8_direct)
-                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, cs));
+                    HIP_TRY(hipMemcpyAsync(a->out_srgb8, u8_src, (size_t)u8_bytes, hipMemcpyDeviceToHost, cs));
                 if (a->out_rgb && !rgb_direct)
                     HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, cs));
                 if (c->use_copy_stream) {
@@ -3243,7 +3345,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!sharded && a->out_rgb && !rgb_direct)
             HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, c->f->stream));
         if (!sharded && a->out_srgb8 && !u8_direct)
-            HIP_TRY(hipMemcpyAsync(a->out_srgb8, c->f->u8, (size_t)3 * npix, hipMemcpyDeviceToHost, c->f->stream));
+            HIP_TRY(hipMemcpyAsync(a->out_srgb8, u8_src, (size_t)u8_bytes, hipMemcpyDeviceToHost, c->f->stream));
         c->f->dirty = true;
         HIP_TRY(hipStreamSynchronize(c->f->stream));
         c->f->dirty = false;
@@ -3359,7 +3461,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
         P.fb = c->f->fb;
         P.fbx = fx ? c->f->fbx : nullptr;
         P.npix = n;
-        const Variant& V = pick_variant(c->mats);
+        const Variant& V = pick_variant(c->mats, c->seq_on ? c->seq : 0);
         for (int d = d0; d <= dlast; ++d) {
             P.depth = d;
             P.qin = c->f->q[d & 1];
@@ -3969,8 +4071,10 @@ int srt_debug_mt_residue(srt_ctx* c, int64_t* nonzero_words) {
         for (uint32_t w : h) nz += w != 0u;
         return SRT_OK;
     };
+    // (window 0 of a table holds a copy of the key, written by a plain store at every generation that
+    // jumps -- never an XOR target -- and left there when no segment starts at the key: not counted)
     for (FrameSlot& f : c->slots)
-        if (f.mt_win && (rc = count(f.mt_win, f.mt_win_cap))) return rc;
+        if (f.mt_win && f.mt_win_cap > rtmt::N && (rc = count(f.mt_win + rtmt::N, f.mt_win_cap - rtmt::N))) return rc;
     if (c->mt && (rc = count(mt_end_acc(c), rtmt::N + 1))) return rc;
     *nonzero_words = nz;
     return SRT_OK;

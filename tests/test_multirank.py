@@ -518,3 +518,53 @@ def test_gpu_many_shard_shapes_keep_band_mode_exact():
             assert np.array_equal(out[0][1], out[1][1])
     finally:
         _set_option("mt_bands", 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_gpu_rehearsed_rank0_assembly_places_its_rows(world):
+    """Option rehearse_assemble (bench.py --shard-of N --rehearse-assemble): rank 0's rows of an N-rank
+    frame rendered on one card also run rank 0's k_assemble over its tile and N - 1 stand-in tiles
+    (zeros) and hand back the whole frame: rank 0's rows equal the single-GPU frame's rows, every other
+    row is the stand-ins' zeros.  Other rows sets (not rank 0's) hand back their own tile."""
+    import ctypes
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+    from sightpy._shard import shard_rows
+
+    W, H, spp = 160, 96, 2
+    sc = scenes.example1(W, H, 3)
+    np.random.seed(8)
+    full = B.render_scene(sc, spp, seed=5, mt=True)
+    lib, ctx = B.context()
+    N.check(lib, lib.srt_set_option(ctx, b"rehearse_assemble", world))
+    try:
+        rows0 = shard_rows(H, world, 0)
+        np.random.seed(8)
+        B.upload(sc)
+        cd = B.camera_desc(sc.camera)
+        r32 = np.ascontiguousarray(rows0, dtype=np.int32)
+        mt = N.MtState.from_numpy()
+        a = N.RenderArgs()
+        a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, len(r32), 0
+        a.rows, a.jitter, a.out_hit_id, a.seed = N.ptr(r32), None, None, 5
+        a.mt = ctypes.pointer(mt)
+        out = B.pinned_buffer("rehearse_u8", 3 * W * H)
+        out[:] = 7
+        a.out_srgb8, a.out_rgb = out.ctypes.data, None
+        a.flags = N.RENDER_ASYNC | N.RENDER_RGB_LOCAL
+        N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+        N.check(lib, lib.srt_render_finish(ctx, None))
+        img = out.reshape(H, W, 3).copy()
+        mask = np.zeros(H, dtype=bool)
+        mask[rows0] = True
+        assert np.array_equal(img[mask], full.srgb8[mask])
+        assert not img[~mask].any()
+        # rank 1's rows: no assembly, its own tile
+        rows1 = shard_rows(H, world, 1)
+        np.random.seed(8)
+        part = B.render_scene(sc, spp, seed=5, mt=True, rows=rows1)
+        assert np.array_equal(part.srgb8, full.srgb8[rows1])
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"rehearse_assemble", 0))
