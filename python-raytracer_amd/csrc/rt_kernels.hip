@@ -1130,6 +1130,9 @@ const Variant VARIANTS[] = {
 // Variants for scenes of a given collider sequence (rt_device.h seq_of: the colliders intersected in
 // straight-line code); a scene runs one when its colliders have exactly these types in this order
 // and its materials are covered.
+#ifndef RT_NO_SEQ_VARIANTS
+#define RT_SEQ_VARIANTS
+#endif
 #ifdef RT_SEQ_VARIANTS
 constexpr uint32_t seq_bits(std::initializer_list<int> t) {
     uint32_t q = (uint32_t)t.size();
@@ -1137,7 +1140,8 @@ constexpr uint32_t seq_bits(std::initializer_list<int> t) {
     for (int v : t) q |= (uint32_t)v << (4 + 2 * k++);
     return q << SEQ_SHIFT;
 }
-// example1 / the headline: two spheres, a plane, the sky box
+// example1 / the headline: two spheres, a plane, the sky box (same box, ex1 1080p d5 6 spp: device-
+// resident frame 0.837 -> 0.750 ms, k_primary 1.05 -> 0.95 ms; profiles/r05_collider_seq_ab.txt)
 constexpr uint32_t MATS_SEQ_SSPC = MATS_GLOSSY_SKY | seq_bits({SRT_SPHERE, SRT_SPHERE, SRT_PLANE, SRT_CUBOID});
 const Variant SEQ_VARIANTS[] = {
     {MATS_SEQ_SSPC, k_primary<MATS_SEQ_SSPC, OCC>, k_trace<MATS_SEQ_SSPC, OCC>, k_frame<MATS_SEQ_SSPC, OCC>,
@@ -1573,6 +1577,9 @@ struct srt_ctx {
     // frame's latency: 2^19-word tabulated segments 0.42 ms, 2^17-word ones ~0.1 ms for 4x the jumps,
     // made in band mode (host jump polynomials, cached per frame shape); 0: tabulated segments
     int64_t mt_short = 65536;
+    // option "mt_short_all": pipelined whole frames take the short segments too (their generation's
+    // latency, not only the first frame's, then shrinks, for four times the jumps)
+    bool mt_short_all = false;
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
@@ -1605,11 +1612,17 @@ struct srt_ctx {
     // 0.20 / 0.33 / 0.21, profiles/r04_mt_stream_ab.txt); 0 the frame's stream; 1 a stream of its own;
     // 2 a high-priority one
     int use_mt_stream = -1;
-    // option "mt_gen_stream": with the generation on the MT stream (whole pipelined frames), 1 runs a
-    // frame's generators on the frame's own stream after its jump kernel (event): the MT stream then
-    // carries only the chain of jump kernels (each makes the next frame's key), and frame k+1's jumps
-    // do not wait behind frame k's generators; 0 keeps jumps and generators in one stream order
-    int mt_gen_stream = 1;
+    // option "mt_gen_stream": where the generators of a whole pipelined frame run when its jump kernel
+    // makes the next frame's key (frame-end jump).  0: after the jump kernel on the MT stream (frame
+    // k+1's jumps then wait behind frame k's generators: the chain jump + generators, ~1 ms under
+    // load, paces the frames); 1: on the frame's own stream (normal priority); 2: on two
+    // high-priority generator streams taken in turn, so the MT stream carries only the jump chain
+    // and consecutive frames' generators overlap
+    // (same box, ex1 1080p pipelined frames, ms: 0 0.940, 1 ~1.05, 2 1.014-1.028 with seven hardware
+    // queues, 0.95-0.96 with nine; profiles/r05_mt_generator_ab.txt)
+    int mt_gen_stream = 0;
+    hipStream_t gen_streams[2] = {nullptr, nullptr};
+    int gen_next = 0;
     bool use_copy_stream = false;
     // option "deterministic" (default 1): contributions added to a pixel by other threads go into
     // order-independent fixed-point sums (bit-reproducible frames); 0: f64 atomics
@@ -1922,6 +1935,7 @@ int mt_end_reset(srt_ctx* c) {
 int mt_jump_parts(const srt_ctx* c) { return c->mt_parts_opt ? c->mt_parts_opt : 4; }
 
 
+
 // The y words of `key` for a generation on `st`: those an end block made with the key (a final
 // window), else k_mt_y into the scratch buffer (one workgroup, ~34 blocks).  Generations of
 // different frames are ordered by the key they hand on, so one scratch buffer suffices.
@@ -2046,7 +2060,8 @@ int mt_band_table(srt_ctx* c, int64_t W, int64_t Hf, int ns, int plane_mask, con
 // the final window (next key) and its y come from the jump kernel's end block.
 int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, int pos, int64_t n_words,
                     const srt_ctx::MtBandTab& T, double* out, int* final_pos, const uint32_t* end_poly,
-                    hipEvent_t key_ready, hipStream_t gst = nullptr, hipEvent_t jumped = nullptr) {
+                    hipEvent_t key_ready, hipStream_t gst = nullptr, hipEvent_t jumped = nullptr,
+                    hipStream_t* gen_on = nullptr) {
     const int64_t abs_end = pos + n_words;
     const int64_t dump_abs = ((abs_end + rtmt::N - 1) / rtmt::N - 1) * rtmt::N;
     MtArgs A{};
@@ -2089,6 +2104,7 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     }
     hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, gst, G, win);
     HIP_TRY(hipGetLastError());
+    if (gen_on) *gen_on = gst;
     c->mt_dirty = false;
     c->mt_y_valid[c->mt_cur ^ 1] = true;
     c->mt_cur ^= 1;
@@ -2107,7 +2123,8 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
 int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, int pos, int64_t n_out, int64_t n_skip,
               double* out, int* final_pos, int64_t plane = 0, int plane_mask = 15, const uint32_t* end_poly = nullptr,
               int64_t end_at = 0, hipEvent_t key_ready = nullptr, hipStream_t gst = nullptr,
-              hipEvent_t jumped = nullptr) {
+              hipEvent_t jumped = nullptr, hipStream_t* gen_on = nullptr) {
+    if (gen_on) *gen_on = st;
     uint32_t* keys[2] = {c->mt + MT_NTAB, c->mt + MT_NTAB + rtmt::N};
     const rtmt::Plan plan = rtmt::make_plan(pos, 2 * (n_out + n_skip));
     if (plan.rounds.size() != 1) end_poly = nullptr;
@@ -2165,6 +2182,7 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
         }
         hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, g, G, win);
         HIP_TRY(hipGetLastError());
+        if (gen_on) *gen_on = g;
         c->mt_dirty = false;
     }
     c->mt_cur ^= 1;
@@ -2449,6 +2467,8 @@ int srt_destroy(srt_ctx* c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->mt_done) (void)hipEventDestroy(c->mt_done);
     if (c->mt_stream) (void)hipStreamDestroy(c->mt_stream);
+    for (hipStream_t g : c->gen_streams)
+        if (g) (void)hipStreamDestroy(g);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_y};
     for (void* p : bufs)
@@ -2469,8 +2489,13 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
-    if (!strcmp(key, "mt_gen_stream")) { c->mt_gen_stream = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_gen_stream")) {
+        if (value < 0 || value > 2) return fail(SRT_ERR_ARG, "mt_gen_stream: 0, 1 or 2");
+        c->mt_gen_stream = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "collider_seq")) { c->seq_on = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_short_all")) { c->mt_short_all = value != 0; return SRT_OK; }
     if (!strcmp(key, "rehearse_assemble")) {
         if (value != 0 && (value < 2 || value > MAX_RANKS)) return fail(SRT_ERR_ARG, "rehearse_assemble: 0 or 2 .. 64");
         c->rehearse_assemble = (int)value;
@@ -2887,7 +2912,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // a whole frame with nothing in flight (synchronous, or the first of a pipeline): short segments in
     // band mode (srt_ctx::mt_short); later pipelined frames generate behind their predecessors
     // (tabulated 2^19-word segments, fewer jumps)
-    const bool mt_short = use_mt && c->mt_bands_on && c->mt_short > 0 && n_rows == Hf && c->async_pending == 0;
+    const bool mt_short = use_mt && c->mt_bands_on && c->mt_short > 0 && n_rows == Hf &&
+                          (c->async_pending == 0 || c->mt_short_all);
     if (use_mt && c->mt_bands_on && (n_rows < Hf || mt_short)) {
         const int last_ns = a->spp - (F.npass - 1) * batch;
         const int64_t split = n_rows < Hf ? (int64_t)1 << 18 : c->mt_short;
@@ -3120,21 +3146,34 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                 const uint32_t* end_poly = nullptr;
                 if (end && (rc = mt_end_poly_for(c, n_words, &end_poly))) return rc;
                 // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
-                // (a pipelined whole frame's generators on its own stream: see srt_ctx::mt_gen_stream)
-                hipStream_t gst = (mst != c->f->stream && c->mt_gen_stream && end) ? c->f->stream : mst;
+                // (a pipelined whole frame's generators off the jump chain: see srt_ctx::mt_gen_stream)
+                hipStream_t gst = mst;
+                if (mst != c->f->stream && end && c->mt_gen_stream == 1) gst = c->f->stream;
+                if (mst != c->f->stream && end && c->mt_gen_stream == 2) {
+                    hipStream_t& g = c->gen_streams[c->gen_next];
+                    if (!g) {
+                        int lo = 0, hi = 0;
+                        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                        HIP_TRY(hipStreamCreateWithPriority(&g, hipStreamNonBlocking, hi));
+                    }
+                    gst = g;
+                    c->gen_next ^= 1;
+                }
+                hipStream_t gen_on = mst;
                 if (band) {
                     if ((rc = mt_launch_bands(c, mst, c->f->mt_win, mt_key, mt_pos, n_words, *bt, c->f->jit, &mt_pos,
-                                              end_poly, p + 1 == F.npass ? c->mt_done : nullptr, gst, c->f->mt_jumped)))
+                                              end_poly, p + 1 == F.npass ? c->mt_done : nullptr, gst, c->f->mt_jumped,
+                                              &gen_on)))
                         return rc;
                 } else if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos,
                                            W * Hf, mt_pm, end_poly, end ? (int64_t)rtmt::end_jump(n_words) : 0,
-                                           end ? c->mt_done : nullptr, gst, c->f->mt_jumped))) {
+                                           end ? c->mt_done : nullptr, gst, c->f->mt_jumped, &gen_on))) {
                     return rc;
                 }
                 // otherwise the next frame's stream may start as soon as this one's is generated
                 if (p + 1 == F.npass && !end) HIP_TRY(hipEventRecord(c->mt_done, mst));
-                if (mst != c->f->stream) {
-                    HIP_TRY(hipEventRecord(c->f->jit_ready, mst));
+                if (gen_on != c->f->stream) {
+                    HIP_TRY(hipEventRecord(c->f->jit_ready, gen_on));
                     HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->jit_ready, 0));
                 }
                 P.jitter = c->f->jit;

@@ -12,6 +12,11 @@
 
 namespace rtmt_dev {
 
+// wave priority of the generation kernels (s_setprio 0..3; 0 = the default, the trace waves' level)
+#ifndef MT_WAVE_PRIO
+#define MT_WAVE_PRIO 0
+#endif
+
 struct MtArgs {
     const uint32_t* key;   // the round's key window (624 words)
     const uint32_t* tab;   // jump polynomials x^(sL-1), s = 1..SEGS-1 (624 words each)
@@ -214,6 +219,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_y(const uint32_t* key, uint32
 // to the y of that window (A.y_next), so the next frame's jump blocks need no k_mt_y.  Block 0 also
 // copies the key window to win[0] for the generators that start from it.
 __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win) {
+    if (MT_WAVE_PRIO) __builtin_amdgcn_s_setprio(MT_WAVE_PRIO);
     extern __shared__ uint32_t mt_lds[];  // mt_jump_lds_words(A.parts)
     __shared__ int last_part;
     uint32_t* yl = mt_lds;                    // this part's slice of y
@@ -336,6 +342,8 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
 template <int NT>
 __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, uint32_t* win) {
     __shared__ uint32_t ring[3 * rtmt::N];
+    // (experiment: the generator's waves ahead of the trace waves they share the SIMDs with)
+    if (MT_WAVE_PRIO) __builtin_amdgcn_s_setprio(MT_WAVE_PRIO);
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const MtSeg g = mt_seg(A, s);
