@@ -261,6 +261,10 @@ typedef struct srt_render_args {
  * Scene.render keeps (the reference returns only the uint8 image, scene.py:118-140): the whole RGB
  * is computed and stored, nothing crosses PCIe or xGMI but the uint8 image. */
 #define SRT_RENDER_RGB_LOCAL 16
+/* SRT_RENDER_RGBX (not with SRT_RENDER_SHARDED): out_srgb8 receives 4-byte pixels [n_rows*width][4]
+ * (R, G, B, 255) instead of 3-byte ones -- PIL's in-memory layout of an RGB image, so that
+ * Scene.render's PIL image is built by a word copy per pixel */
+#define SRT_RENDER_RGBX 32
 
 #define SRT_MAX_DEPTHS 64
 typedef struct srt_stats {

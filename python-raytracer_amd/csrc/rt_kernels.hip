@@ -1378,6 +1378,13 @@ __global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, i
     }
 }
 
+// SRT_RENDER_RGBX: the uint8 image as 4-byte pixels (R, G, B, 255) -- PIL's own layout of an "RGB"
+// image, which it then takes in with a word copy per pixel instead of unpacking 3-byte pixels
+__global__ __launch_bounds__(BLOCK) void k_rgbx(const uint8_t* rgb, uint32_t* rgbx, int64_t npix) {
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < npix; i += (int64_t)gridDim.x * BLOCK)
+        rgbx[i] = (uint32_t)rgb[3 * i] | ((uint32_t)rgb[3 * i + 1] << 8) | ((uint32_t)rgb[3 * i + 2] << 16) | 0xFF000000u;
+}
+
 std::vector<int32_t> band_rows(int64_t H, int n, int q, int64_t band, int snake) {
     std::vector<int32_t> r;
     for (int64_t y = 0; y < H; ++y)
@@ -2782,8 +2789,10 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
     if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS |
-                     SRT_RENDER_RGB_LOCAL))
+                     SRT_RENDER_RGB_LOCAL | SRT_RENDER_RGBX))
         return fail(SRT_ERR_ARG, "unknown render flag");
+    if ((a->flags & SRT_RENDER_RGBX) && (a->flags & SRT_RENDER_SHARDED))
+        return fail(SRT_ERR_ARG, "SRT_RENDER_RGBX: not with SRT_RENDER_SHARDED");
     if ((a->flags & SRT_RENDER_RGB_LOCAL) && (a->out_rgb || (a->flags & (SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS))))
         return fail(SRT_ERR_ARG, "SRT_RENDER_RGB_LOCAL needs out_rgb NULL and no SRT_RENDER_GATHER_RGB / RGB_ROWS");
     if ((a->flags & SRT_RENDER_RGB_ROWS) &&
@@ -2936,7 +2945,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // rank 0's assembly rehearsed (srt_ctx::rehearse_assemble): these rows are rank 0's of an n-rank job
     int reh_n = 0;
     int64_t reh_band = 1, reh_maxpix = 0;
-    if (c->rehearse_assemble > 1 && !sharded && a->rows && a->out_srgb8 && ptr_kind(a->out_srgb8) != 1) {
+    if (c->rehearse_assemble > 1 && !sharded && a->rows && a->out_srgb8 && ptr_kind(a->out_srgb8) != 1 &&
+        !(a->flags & SRT_RENDER_RGBX)) {
         const int n = c->rehearse_assemble;
         reh_band = shard_band_height(Hf, n, shard_kmax(Hf, n, c->shard_bands, c->fanout), c->shard_snake);
         const std::vector<int32_t> r0 = band_rows(Hf, n, 0, reh_band, c->shard_snake);
@@ -2959,6 +2969,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                           F.groups == pp.groups && (F.groups == 1 || (int64_t)F.groups * 3 * npix <= c->f->fbg_cap) &&
                           F.sharded == pp.sharded && F.gather_rgb == pp.gather_rgb && F.use_mt == pp.use_mt &&
                           (!reh_n || (c->f->g_u8_cap >= reh_n * reh_maxpix * 3 && c->f->full_u8_cap >= 3 * W * Hf)) &&
+                          (!(a->flags & SRT_RENDER_RGBX) || c->f->full_u8_cap >= 4 * npix) &&
                           (!sharded || c->rank != 0 ||
                            (c->f->g_u8_cap >= c->nranks * maxpix * 3 && c->f->full_u8_cap >= 3 * W * Hf &&
                             (!gather_rgb || (c->f->g_rgb_cap >= c->nranks * maxpix * 3 && c->f->full_rgb_cap >= 3 * W * Hf)))) &&
@@ -2997,6 +3008,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         if (!r && jit_doubles > 0) r = ensure_buf(&c->f->jit, c->f->jit_cap, jit_doubles);
         if (!r && use_mt) r = mt_win_ensure(c, *c->f, mt_win_need);
         if (!r && a->out_hit_id && !hit_dev) r = ensure_buf(&c->f->hit, c->f->hit_cap, (int64_t)batch * npix);
+        if (!r && (a->flags & SRT_RENDER_RGBX)) r = ensure_buf(&c->f->full_u8, c->f->full_u8_cap, 4 * npix);
         if (!r && reh_n) {
             const int64_t had = c->f->g_u8_cap;
             r = ensure_buf(&c->f->g_u8, c->f->g_u8_cap, reh_n * reh_maxpix * 3);
@@ -3056,7 +3068,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     double* res_rgb = rgb_local ? c->f->rgb
                     : sharded ? ((gather_rgb || rgb_rows) ? c->f->rgb : nullptr)
                               : a->out_rgb ? (rgb_direct ? a->out_rgb : c->f->rgb) : nullptr;
-    uint8_t* res_u8 = sharded ? c->f->u8 : a->out_srgb8 ? (u8_direct ? a->out_srgb8 : c->f->u8) : nullptr;
+    const bool rgbx = (a->flags & SRT_RENDER_RGBX) && a->out_srgb8;
+    uint8_t* res_u8 = (sharded || rgbx) ? c->f->u8 : a->out_srgb8 ? (u8_direct ? a->out_srgb8 : c->f->u8) : nullptr;
     // only the depths this frame can reach are handed back and cleared per pass
     const int64_t used_words = std::min<int64_t>(F.cnt_words, (int64_t)(F.dcap + 2) * NSHARD);
     // the numpy stream continues on the device from the previous asynchronous frame (same `mt`)
@@ -3350,6 +3363,14 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             HIP_TRY(hipGetLastError());
             u8_src = c->f->full_u8;
             u8_bytes = 3 * W * Hf;
+        }
+        if (rgbx) {
+            uint32_t* dst4 = reinterpret_cast<uint32_t*>(u8_direct ? a->out_srgb8 : c->f->full_u8);
+            hipLaunchKernelGGL(k_rgbx, dim3(grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->u8, dst4,
+                               npix);
+            HIP_TRY(hipGetLastError());
+            u8_src = c->f->full_u8;
+            u8_bytes = 4 * npix;
         }
         if (async) {
             // (a synchronous frame gathers after its retries: every rank gathers each frame once)

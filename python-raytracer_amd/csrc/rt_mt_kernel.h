@@ -12,9 +12,12 @@
 
 namespace rtmt_dev {
 
-// wave priority of the generation kernels (s_setprio 0..3; 0 = the default, the trace waves' level)
+// wave priority of the generation kernels (s_setprio 0..3; the trace waves run at 0): a generator
+// workgroup placed on a CU beside trace blocks issues ahead of them, finishes sooner and hands the
+// CU's trace slot back sooner.  Same box, ex1 1080p pipelined frames: 0.938 -> 0.903 ms at 3
+// (profiles/r05_mt_generator_ab.txt)
 #ifndef MT_WAVE_PRIO
-#define MT_WAVE_PRIO 0
+#define MT_WAVE_PRIO 3
 #endif
 
 struct MtArgs {
@@ -342,8 +345,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mt_jump(MtArgs A, uint32_t* win)
 template <int NT>
 __global__ __launch_bounds__(NT) void k_mt_gen(MtArgs A, uint32_t* win) {
     __shared__ uint32_t ring[3 * rtmt::N];
-    // (experiment: the generator's waves ahead of the trace waves they share the SIMDs with)
-    if (MT_WAVE_PRIO) __builtin_amdgcn_s_setprio(MT_WAVE_PRIO);
+    if (MT_WAVE_PRIO) __builtin_amdgcn_s_setprio(MT_WAVE_PRIO);  // (ahead of the trace waves)
     const int s = blockIdx.x;
     const int lane = threadIdx.x;
     const MtSeg g = mt_seg(A, s);

@@ -206,14 +206,15 @@ def _default_seed():
 
 
 def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False,
-                 jitter_device=None, mt=False, pinned_u8=False):
+                 jitter_device=None, mt=False, pinned_u8=False, rgbx=False):
     """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG;
     `jitter_device`: the same uniforms already in device memory (numpy_uniforms); `mt=True`: the
     jitter is numpy's global stream generated on the device (the reference's draws, including the
     sizing draw of scene.py:81), and numpy's global state is advanced past it.  `pinned_u8`: the
     uint8 image lands in the context's pinned host buffer (a view, valid until the next such call)
     instead of a new array.  Without `want_rgb` the linear RGB is resolved and kept in HBM
-    (SRT_RENDER_RGB_LOCAL), as the reference keeps it internal."""
+    (SRT_RENDER_RGB_LOCAL), as the reference keeps it internal.  `rgbx`: the image as 4-byte pixels
+    (R, G, B, 255; SRT_RENDER_RGBX), srgb8 of shape (rows, W, 4)."""
     lib, ctx = context()
     upload(scene)
     cam = scene.camera
@@ -244,17 +245,18 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
         state = N.MtState.from_numpy()
         a.mt = ctypes.pointer(state)
     rgb = np.empty((3, npix)) if want_rgb else None
-    u8 = (pinned_buffer("render_u8", 3 * npix) if pinned_u8 else np.empty(3 * npix, dtype=np.uint8)).reshape(npix, 3)
+    ch = 4 if rgbx else 3
+    u8 = (pinned_buffer("render_u8", ch * npix) if pinned_u8 else np.empty(ch * npix, dtype=np.uint8)).reshape(npix, ch)
     hits = np.empty((spp, npix), dtype=np.int32) if want_hits else None
     a.out_rgb = N.ptr(rgb)
     a.out_srgb8 = N.ptr(u8)
     a.out_hit_id = N.ptr(hits)
-    a.flags = 0 if want_rgb else N.RENDER_RGB_LOCAL
+    a.flags = (0 if want_rgb else N.RENDER_RGB_LOCAL) | (N.RENDER_RGBX if rgbx else 0)
     st = N.Stats()
     N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
     if state is not None:
         state.to_numpy()
-    return RenderResult(u8.reshape(nrows, W, 3), rgb, hits, st.as_dict())
+    return RenderResult(u8.reshape(nrows, W, ch), rgb, hits, st.as_dict())
 
 
 def render_group(scene, spp, seed=None, batch_size=None, want_rgb=True, mt=True):

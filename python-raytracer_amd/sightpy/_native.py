@@ -209,7 +209,7 @@ class TraceArgs(ctypes.Structure):
 
 
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
-RENDER_ASYNC, RENDER_SHARDED, RENDER_GATHER_RGB, RENDER_RGB_ROWS, RENDER_RGB_LOCAL = 1, 2, 4, 8, 16  # SRT_RENDER_*
+RENDER_ASYNC, RENDER_SHARDED, RENDER_GATHER_RGB, RENDER_RGB_ROWS, RENDER_RGB_LOCAL, RENDER_RGBX = 1, 2, 4, 8, 16, 32  # SRT_RENDER_*
 ABI_VERSION = 5  # SRT_ABI_VERSION of include/sightpy_rt.h
 COMM_ID_BYTES = 128
 

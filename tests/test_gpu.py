@@ -692,3 +692,40 @@ def test_gpu_chain_mode_recovers_from_ties(tmp_path):
         assert out.stats["rays_per_depth"] == [counts["depth"][d] for d in sorted(counts["depth"])]
         np.testing.assert_allclose(out.rgb, rgb, rtol=RTOL, atol=ATOL)
     assert all(out.stats["retries"] <= 1 for out in outs)
+
+
+def test_gpu_rgbx_output_is_the_uint8_image_with_opaque_alpha():
+    """SRT_RENDER_RGBX (Scene.render's output path, PIL's own RGB layout): the same pixels as the
+    3-byte image, alpha 255, into pageable, pinned and device memory; Scene.render returns a mode-RGB
+    image equal to the one built from the 3-byte pixels."""
+    import ctypes
+    from PIL import Image
+    from sightpy import _native as N
+
+    B = _backend()
+    sc = scenes.example1(160, 90, 3)
+    np.random.seed(2)
+    jit = sc.camera.draw_jitter(2)
+    ref = B.render_scene(sc, 2, jitter=jit, seed=1)
+    got = B.render_scene(sc, 2, jitter=jit, seed=1, want_rgb=False, rgbx=True)
+    assert got.srgb8.shape == (90, 160, 4)
+    assert np.array_equal(got.srgb8[..., :3], ref.srgb8) and np.all(got.srgb8[..., 3] == 255)
+    pin = B.render_scene(sc, 2, jitter=jit, seed=1, want_rgb=False, rgbx=True, pinned_u8=True)
+    assert np.array_equal(pin.srgb8, got.srgb8)
+    lib, ctx = B.context()
+    d = B.device_buffer("rgbx_out", 4 * 160 * 90)
+    cd = B.camera_desc(sc.camera)
+    a = N.RenderArgs()
+    a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, 90, 0
+    a.rows, a.out_hit_id, a.mt, a.seed = None, None, None, 1
+    jd = np.ascontiguousarray(jit)
+    a.jitter = N.ptr(jd)
+    a.out_rgb, a.out_srgb8 = None, d
+    a.flags = N.RENDER_RGB_LOCAL | N.RENDER_RGBX
+    N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+    h = np.empty((90, 160, 4), dtype=np.uint8)
+    N.check(lib, lib.srt_memcpy(ctx, N.ptr(h), d, h.nbytes))
+    assert np.array_equal(h, got.srgb8)
+    np.random.seed(2)
+    img = sc.render(2, rng="numpy-host", seed=1)
+    assert img.mode == "RGB" and np.array_equal(np.asarray(img), ref.srgb8)
