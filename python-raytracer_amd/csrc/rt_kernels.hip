@@ -1114,6 +1114,7 @@ constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (regi
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
      k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>},
+#ifndef RT_EXP_MIN  // (register-usage experiments, tools/resource_usage.py: the headline variants only, a quicker compile)
     {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
     {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
@@ -1126,6 +1127,7 @@ const Variant VARIANTS[] = {
     // scenes with a triangle BVH (TriangleMesh)
     {MAT_GENERIC | MAT_BVH, k_primary<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC>,
      k_frame<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC, true>},
+#endif
 };
 // Variants for scenes of a given collider sequence (rt_device.h seq_of: the colliders intersected in
 // straight-line code); a scene runs one when its colliders have exactly these types in this order

@@ -204,13 +204,54 @@ def _fingerprint(a):
     return fp
 
 
+# Memo of the pure per-material expressions below (each ~15-20 us of numpy scalar/vec3 arithmetic,
+# evaluated on every Scene.render): keyed by the operands' types and exact values (repr keeps -0.0
+# and nan apart), so a memo hit returns what the expression would.  Operands that are not Python or
+# numpy scalars / small arrays are not memoised.
+_EXPR_MEMO = {}
+_EXPR_MEMO_MAX = 4096
+
+
+def _vkey(v):
+    """Exact key of a scalar or small array operand, or None."""
+    if isinstance(v, (float, complex, int)) and not isinstance(v, bool):
+        return (type(v).__name__, repr(v))
+    if isinstance(v, np.ndarray) and v.size <= 4:
+        return ("nd", v.dtype.str, v.shape, v.tobytes())
+    if isinstance(v, np.generic):
+        return ("np", v.dtype.str, v.tobytes())
+    return None
+
+
+def _memo(tag, operands, fn):
+    keys = tuple(_vkey(v) for v in operands)
+    if any(k is None for k in keys):
+        return fn()
+    key = (tag,) + keys
+    hit = _EXPR_MEMO.get(key)
+    if hit is None:
+        if len(_EXPR_MEMO) >= _EXPR_MEMO_MAX:
+            _EXPR_MEMO.clear()
+        hit = _EXPR_MEMO[key] = fn()
+    return hit
+
+
 def _medium_f0(n_ray, n_mat):
     """|(n_ray - n)/(n_ray + n)|^2 per component with numpy array semantics (glossy.py:66):
     n_ray is a length-1 array of the ray's n dtype, n_mat the material's Python scalars."""
-    out = []
-    for a, b in zip(n_ray, n_mat):
-        out.append(float((np.abs((a - b) / (a + b)) ** 2)[0]))
-    return out
+    def f0():
+        return [float((np.abs((a - b) / (a + b)) ** 2)[0]) for a, b in zip(n_ray, n_mat)]
+
+    return list(_memo("medium_f0", tuple(n_ray) + tuple(n_mat), f0))
+
+
+def _glossy_f0(scene_n, m_n):
+    """np.abs((scene.n - m.n) / (scene.n + m.n)) ** 2 as in glossy.py:91 (vec3 of Python scalars)."""
+    def f0():
+        return _f3(np.abs((scene_n - m_n) / (scene_n + m_n)) ** 2)
+
+    ops = (scene_n.x, scene_n.y, scene_n.z, m_n.x, m_n.y, m_n.z)
+    return list(_memo("glossy_f0", ops, f0))
 
 
 def texture_record(u8, repeat=1.0, linear=True):
@@ -352,8 +393,7 @@ def lower_scene(scene, extra_media=()):
                     r["ival"] = k  # device evaluates x**a as x**k (rt_device.h powi)
             p[6] = 2.0 * np.pi
             p[7] = m.spec_coeff
-            F0 = np.abs((scene.n - m.n) / (scene.n + m.n)) ** 2  # glossy.py:91 (Python scalars)
-            p[8:11] = _f3(F0)
+            p[8:11] = _glossy_f0(scene.n, m.n)  # glossy.py:91 (Python scalars)
             for k, arrs in enumerate(media_arrays):
                 glossy_f0[i, k] = _medium_f0(arrs, [m.n.x, m.n.y, m.n.z])
             p[11:14] = glossy_f0[i, 0]  # medium 0 copy, read with scalar loads

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--config", default="example1_1080p_d5", choices=sorted(CONFIGS))
     ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--profile", action="store_true", help="cProfile one render (host-side breakdown)")
+    ap.add_argument("--phases", action="store_true", help="median ms of the call's steps (lowering, device frame, PIL)")
     ap.add_argument("--option", action="append", default=[], help="srt_set_option KEY=VALUE (repeatable)")
     a = ap.parse_args()
     builder, W, H, depth, spp, label = CONFIGS[a.config]
@@ -55,13 +56,36 @@ def main():
         sc.render(spp)
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(25)
+    phases = None
+    if a.phases:
+        # the same call in its steps (scene.py render): lowering alone, lowering + signature check, the
+        # device frame (render_scene: its own lowering, RGBX image to pinned memory), the PIL image
+        from PIL import Image
+        from sightpy import _backend as B
+
+        acc = {"lower_only": [], "lower_upload": [], "device_frame": [], "pil": []}
+        for _ in range(a.repeats):
+            np.random.seed(0)
+            tl = time.perf_counter()
+            B.lower_scene(sc)
+            t0 = time.perf_counter()
+            B.upload(sc)
+            t1 = time.perf_counter()
+            out = B.render_scene(sc, spp, want_rgb=False, mt=True, pinned_u8=True, rgbx=True)
+            t2 = time.perf_counter()
+            im = Image.new("RGB", (W, H))
+            im.frombytes(out.srgb8, "raw", "RGBX")
+            t3 = time.perf_counter()
+            for k, v in zip(acc, (t0 - tl, t1 - t0, t2 - t1, t3 - t2)):
+                acc[k].append(v)
+        phases = {k: round(float(np.median(v)) * 1e3, 3) for k, v in acc.items()}
     rays = sc.last_stats["total_rays"]
     best, med = min(times), float(np.median(times))
     print(json.dumps({"what": "Scene.render(%d) via the public API, host buffers (PCIe-inclusive)" % spp,
                       "options": a.option,
                       "workload": label, "image": list(img.size), "rays_per_frame": int(rays),
                       "ms_median": round(med * 1e3, 3), "ms_min": round(best * 1e3, 3),
-                      "Mrays_per_s_median": round(rays / med / 1e6, 1), "repeats": a.repeats}))
+                      "Mrays_per_s_median": round(rays / med / 1e6, 1), "repeats": a.repeats, "phases_ms_median": phases}))
 
 
 if __name__ == "__main__":
