@@ -308,6 +308,14 @@ int srt_destroy(srt_ctx* ctx);
 int srt_set_option(srt_ctx* ctx, const char* key, int64_t value);
 int srt_upload_scene(srt_ctx* ctx, const srt_scene_desc* scene);
 int srt_render(srt_ctx* ctx, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);
+/* Queue the numpy-stream generation of the synchronous whole frame that srt_render will be called
+ * for next with the same camera size and args (args->mt set, no rows, not SRT_RENDER_ASYNC /
+ * SHARDED; otherwise it does nothing), so that it runs on the GPU while the caller lowers and uploads
+ * its scene -- reference scene.py:71-83 draws the jitter before the samples are traced.  That
+ * srt_render finds it queued (same stream state, frame shape and options) and does not launch it
+ * again; any other render, option change, srt_trace/srt_shade or srt_mt19937_uniforms call drops it.
+ * Does not advance args->mt (srt_render does).  Needs no scene. */
+int srt_render_prefetch(srt_ctx* ctx, const srt_camera* cam, const srt_render_args* args);
 int srt_render_finish(srt_ctx* ctx, srt_stats* stats);
 /* the hipStream_t every call on ctx is ordered on (for stream/event interop, e.g. torch) */
 int srt_stream(srt_ctx* ctx, void** stream);
@@ -399,6 +407,9 @@ int srt_synchronize(srt_ctx* ctx);
  * XOR targets of the jump parts, all but window 0, the key's copy --, the end-window accumulator and
  * its arrival counter): 0 on a healthy context. */
 int srt_debug_mt_residue(srt_ctx* ctx, int64_t* nonzero_words);
+/* Diagnostic: renders that found their generation queued by srt_render_prefetch (used, not
+ * launched again) and prefetches queued, since the context was created. */
+int srt_debug_prefetch_counts(srt_ctx* ctx, int64_t* used, int64_t* queued);
 const char* srt_last_error(void);
 
 #ifdef __cplusplus

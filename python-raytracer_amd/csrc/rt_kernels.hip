@@ -1680,6 +1680,20 @@ struct srt_ctx {
     // RCCL gather (the transfers themselves are not rehearsed)
     int rehearse_assemble = 0;
     double* red = nullptr;      // srt_comm_allreduce scratch
+    // srt_render_prefetch: the numpy-stream generation of the synchronous whole frame srt_render is
+    // about to be called for, queued before the caller lowers and uploads its scene (Scene.render);
+    // the next srt_render with the same stream state and frame shape finds it queued and skips its
+    // own launch.  Any other call that generates from the stream drops it.
+    struct MtPrefetch {
+        bool valid = false;
+        uint32_t key[rtmt::N];
+        int pos = 0;
+        int64_t shape[8] = {};       // W, H, spp, batch, plane mask, slot, stream, generation flavour
+        const void* bt[2] = {nullptr, nullptr};  // the band tables it used
+        int final_pos = 0;
+        hipStream_t gen_on = nullptr;
+    } pf;
+    int64_t pf_used = 0, pf_queued = 0;  // (srt_debug_prefetch_counts)
 };
 
 namespace {
@@ -2493,6 +2507,7 @@ int srt_destroy(srt_ctx* c) {
 
 int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
+    c->pf.valid = false;  // (an option may change the streams or the generation a prefetch assumed)
     if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
     if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
@@ -2786,10 +2801,16 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
 }
 
 
-int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
+}  // extern "C"
+namespace {
+// srt_render, or with `prefetch` srt_render_prefetch: the same planning, then only the first pass's
+// numpy-stream generation is queued (srt_ctx::pf) and the call returns
+int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_stats* st, bool prefetch) {
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !cam || !a) return fail(SRT_ERR_ARG, "null argument");
-    if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
+    const srt_ctx::MtPrefetch pf_in = c->pf;  // (a prefetch is used by the next render only)
+    c->pf.valid = false;
+    if (!prefetch && !c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
     if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_SHARDED | SRT_RENDER_GATHER_RGB | SRT_RENDER_RGB_ROWS |
                      SRT_RENDER_RGB_LOCAL | SRT_RENDER_RGBX))
         return fail(SRT_ERR_ARG, "unknown render flag");
@@ -2807,6 +2828,8 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     if (a->jitter && a->mt) return fail(SRT_ERR_ARG, "jitter and mt are exclusive");
     const bool use_mt = a->mt != nullptr;
     if (use_mt && (a->mt->pos < 0 || a->mt->pos > rtmt::N)) return fail(SRT_ERR_ARG, "bad numpy RNG position");
+    // a prefetch covers synchronous whole frames drawing numpy's stream (Scene.render); others: nothing
+    if (prefetch && (async || sharded || !use_mt || a->rows || a->n_rows != cam->height)) return SRT_OK;
     // rows of this call
     std::vector<int32_t> rows_h;
     const int32_t* rows_src = nullptr;
@@ -3077,14 +3100,27 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
     // the numpy stream continues on the device from the previous asynchronous frame (same `mt`)
     const bool mt_chained = use_mt && async && c->async_pending > 0 && c->mt_chain == a->mt;
     srt_stats S{};
+    // this frame's first-pass generation already queued by srt_render_prefetch (same stream state,
+    // same frame shape, nothing generated since): not launched again (the first iteration only)
+    bool pf_hit = false;
+    const int mts = use_mt ? (c->use_mt_stream >= 0 ? c->use_mt_stream : (n_rows >= Hf ? 2 : 0)) : 0;
+    const int64_t pf_shape[8] = {W, Hf, a->spp, batch, mt_pm, (int64_t)(c->f - c->slots), mts,
+                                 (int64_t)c->mt_bands_on * 2 + (c->mt_short > 0)};
+    if (prefetch && (F.npass != 1 || !mts)) return SRT_OK;  // (the generation would run on the frame's stream)
+    if (!prefetch && use_mt && pf_in.valid && !async && !sharded && !a->rows && n_rows == Hf && F.npass == 1 && mts &&
+        !memcmp(pf_in.shape, pf_shape, sizeof pf_shape) && pf_in.bt[0] == mt_bt[0] && pf_in.bt[1] == mt_bt[1] &&
+        pf_in.pos == a->mt->pos && !memcmp(pf_in.key, a->mt->key, sizeof pf_in.key))
+        pf_hit = true;
     for (;;) {
-        if (c->f->pending == 0) clear_host_flags(c, F);  // k_pass_end ORs into them
-        if (c->f->dirty) {
-            HIP_TRY(hipMemsetAsync(c->f->shadow, 0, 8 * NSHARD, c->f->stream));
-            HIP_TRY(hipMemsetAsync(c->f->counts, 0, (size_t)F.cnt_words * 4, c->f->stream));
-            HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
+        if (!prefetch) {
+            if (c->f->pending == 0) clear_host_flags(c, F);  // k_pass_end ORs into them
+            if (c->f->dirty) {
+                HIP_TRY(hipMemsetAsync(c->f->shadow, 0, 8 * NSHARD, c->f->stream));
+                HIP_TRY(hipMemsetAsync(c->f->counts, 0, (size_t)F.cnt_words * 4, c->f->stream));
+                HIP_TRY(hipMemsetAsync(c->f->flags, 0, 8, c->f->stream));
+            }
+            c->f->dirty = true;
         }
-        c->f->dirty = true;
         int mt_pos = 0;
         const uint32_t* mt_key = nullptr;
         // the stream the numpy-stream generation runs on: the MT stream for a single-pass frame
@@ -3094,7 +3130,6 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             // (auto: whole frames on the high-priority stream, shards on the frame's stream: a stream
             // shared by the frames serialises their generations, and a shard's band segments -- one
             // serial generator block each -- are long: a rank of 2's 130k-double bands take ~0.4 ms)
-            const int mts = c->use_mt_stream >= 0 ? c->use_mt_stream : (n_rows >= Hf ? 2 : 0);
             if (F.npass == 1 && mts) {
                 if (!c->mt_stream) {
                     // a high-priority queue (mt_stream 2): the generation's blocks are dispatched ahead
@@ -3106,16 +3141,16 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                         HIP_TRY(hipStreamCreateWithFlags(&c->mt_stream, hipStreamNonBlocking));
                 }
                 mst = c->mt_stream;
-                if (c->f->jit_busy) HIP_TRY(hipStreamWaitEvent(mst, c->f->jit_free, 0));
+                if (c->f->jit_busy && !pf_hit) HIP_TRY(hipStreamWaitEvent(mst, c->f->jit_free, 0));
             }
             // this frame's stream starts where the previous frame's ended (device dump window) or at
             // the caller's state
-            if (c->mt_done) HIP_TRY(hipStreamWaitEvent(mst, c->mt_done, 0));
+            if (c->mt_done && !pf_hit) HIP_TRY(hipStreamWaitEvent(mst, c->mt_done, 0));
             if (mt_chained) {
                 mt_key = mt_dump(c);
                 mt_pos = c->mt_pos;
             } else {
-                HIP_TRY(hipMemcpyAsync(mt_key0(c), a->mt->key, rtmt::N * 4, hipMemcpyHostToDevice, mst));
+                if (!pf_hit) HIP_TRY(hipMemcpyAsync(mt_key0(c), a->mt->key, rtmt::N * 4, hipMemcpyHostToDevice, mst));
                 mt_key = mt_key0(c);
                 mt_pos = a->mt->pos;
             }
@@ -3175,18 +3210,39 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
                     c->gen_next ^= 1;
                 }
                 hipStream_t gen_on = mst;
-                if (band) {
-                    if ((rc = mt_launch_bands(c, mst, c->f->mt_win, mt_key, mt_pos, n_words, *bt, c->f->jit, &mt_pos,
-                                              end_poly, p + 1 == F.npass ? c->mt_done : nullptr, gst, c->f->mt_jumped,
-                                              &gen_on)))
+                if (pf_hit && p == 0) {  // queued by srt_render_prefetch
+                    mt_pos = pf_in.final_pos;
+                    gen_on = pf_in.gen_on;
+                    c->pf_used++;
+                } else {
+                    if (band) {
+                        if ((rc = mt_launch_bands(c, mst, c->f->mt_win, mt_key, mt_pos, n_words, *bt, c->f->jit, &mt_pos,
+                                                  end_poly, p + 1 == F.npass ? c->mt_done : nullptr, gst,
+                                                  c->f->mt_jumped, &gen_on)))
+                            return rc;
+                    } else if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos,
+                                               W * Hf, mt_pm, end_poly, end ? (int64_t)rtmt::end_jump(n_words) : 0,
+                                               end ? c->mt_done : nullptr, gst, c->f->mt_jumped, &gen_on))) {
                         return rc;
-                } else if ((rc = mt_launch(c, mst, c->f->mt_win, mt_key, mt_pos, n_out, n_skip, c->f->jit, &mt_pos,
-                                           W * Hf, mt_pm, end_poly, end ? (int64_t)rtmt::end_jump(n_words) : 0,
-                                           end ? c->mt_done : nullptr, gst, c->f->mt_jumped, &gen_on))) {
-                    return rc;
+                    }
+                    // otherwise the next frame's stream may start as soon as this one's is generated
+                    if (p + 1 == F.npass && !end) HIP_TRY(hipEventRecord(c->mt_done, mst));
                 }
-                // otherwise the next frame's stream may start as soon as this one's is generated
-                if (p + 1 == F.npass && !end) HIP_TRY(hipEventRecord(c->mt_done, mst));
+                if (prefetch) {
+                    // queued: the frame's stream waits for it when srt_render comes (a wait queued
+                    // here would also hold up the scene upload's synchronisation of that stream)
+                    srt_ctx::MtPrefetch& q = c->pf;
+                    memcpy(q.key, a->mt->key, sizeof q.key);
+                    q.pos = a->mt->pos;
+                    memcpy(q.shape, pf_shape, sizeof pf_shape);
+                    q.bt[0] = mt_bt[0];
+                    q.bt[1] = mt_bt[1];
+                    q.final_pos = mt_pos;
+                    q.gen_on = gen_on;
+                    q.valid = true;
+                    c->pf_queued++;
+                    return SRT_OK;
+                }
                 if (gen_on != c->f->stream) {
                     HIP_TRY(hipEventRecord(c->f->jit_ready, gen_on));
                     HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->jit_ready, 0));
@@ -3426,6 +3482,7 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
             if ((bits & RETRY_OVERFLOW) &&
                 (rc = F.frame ? ensure_ring(c, 2 * c->f->ring_cap) : ensure_queues(c, 2 * c->f->seg * NSHARD)))
                 return rc;
+            pf_hit = false;  // (the retry generates its stream again from the caller's state)
             continue;
         }
         S.retries = retries;
@@ -3445,6 +3502,16 @@ int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_
         *st = S;
     }
     return SRT_OK;
+}
+}  // namespace
+
+extern "C" {
+int srt_render(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt_stats* st) {
+    return render_impl(c, cam, a, st, false);
+}
+
+int srt_render_prefetch(srt_ctx* c, const srt_camera* cam, const srt_render_args* a) {
+    return render_impl(c, cam, a, nullptr, true);
 }
 
 int srt_render_finish(srt_ctx* c, srt_stats* st) {
@@ -3467,6 +3534,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
                srt_stats* st) {
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !a || !a->origin || !a->dir || !a->out_rgb) return fail(SRT_ERR_ARG, "null argument");
+    c->pf.valid = false;  // (slot 0's buffers are reused here)
     if (!c->has_scene) return fail(SRT_ERR_NOSCENE, "no scene uploaded");
     if (a->depth < 0 || a->depth > 200 || a->diffuse_reflections < 0) return fail(SRT_ERR_ARG, "bad depth");
     if (a->n <= 0) return SRT_OK;
@@ -3816,6 +3884,7 @@ int srt_memcpy(srt_ctx* c, void* dst, const void* src, int64_t bytes) {
 int srt_mt19937_uniforms(srt_ctx* c, const uint32_t* key, int32_t pos, int64_t n_out, int64_t n_skip, double* out,
                          uint32_t* key_out, int32_t* pos_out) {
     if (!c || !key || !key_out || !pos_out || (n_out > 0 && !out)) return fail(SRT_ERR_ARG, "null argument");
+    c->pf.valid = false;  // (generates from the stream state a prefetch assumed)
     if (pos < 0 || pos > rtmt::N || n_out < 0 || n_skip < 0) return fail(SRT_ERR_ARG, "bad position or count");
     if (is_device_ptr(key) || is_device_ptr(key_out)) return fail(SRT_ERR_ARG, "key and key_out are host arrays");
     if (n_out + n_skip == 0) {
@@ -3909,6 +3978,7 @@ int srt_render_group(srt_ctx** ctxs, int n, const srt_camera* cam, const srt_ren
     for (int q = 0; q < n; ++q)
         if (!ctxs[q] || ctxs[q]->nranks != n || ctxs[q]->rank != q)
             return fail(SRT_ERR_ARG, "contexts must be the ranks 0..n-1 of one srt_comm_init_all group");
+    for (int q = 0; q < n; ++q) ctxs[q]->pf.valid = false;
     if (a->jitter) return fail(SRT_ERR_ARG, "a group frame draws its jitter on the devices (mt or Philox)");
     if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
     if (a->flags & ~(SRT_RENDER_ASYNC | SRT_RENDER_RGB_ROWS | SRT_RENDER_RGB_LOCAL))
@@ -4118,6 +4188,13 @@ int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
     return SRT_OK;
 }
 #endif
+
+int srt_debug_prefetch_counts(srt_ctx* c, int64_t* used, int64_t* queued) {
+    if (!c || !used || !queued) return fail(SRT_ERR_ARG, "null argument");
+    *used = c->pf_used;
+    *queued = c->pf_queued;
+    return SRT_OK;
+}
 
 int srt_debug_mt_residue(srt_ctx* c, int64_t* nonzero_words) {
     if (!c || !nonzero_words) return fail(SRT_ERR_ARG, "null argument");

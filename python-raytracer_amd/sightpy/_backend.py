@@ -145,6 +145,79 @@ def pinned_buffer(name, nbytes):
     return np.ctypeslib.as_array(ctypes.cast(cur[0], ctypes.POINTER(ctypes.c_uint8)), (cur[1],))[:nbytes]
 
 
+class _HostBlock:
+    """A pinned host allocation of the context lent to numpy as the base of one array (and through it
+    to a PIL image mapping that array): when the last of them is gone the allocation goes back to a
+    small pool for the next image (image_block)."""
+
+    __slots__ = ("ptr", "nbytes")
+
+    def __init__(self, ptr, nbytes):
+        self.ptr, self.nbytes = ptr, nbytes
+
+    @property
+    def __array_interface__(self):
+        return {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.ptr, False), "version": 3}
+
+    def __del__(self):
+        try:
+            _STATE["blocks_out"] -= 1
+            free = _STATE["blocks"].setdefault(self.nbytes, [])
+            if len(free) < _BLOCKS_FREE_MAX and _STATE["ctx"] is not None:
+                free.append(self.ptr)
+            elif _STATE["ctx"] is not None:
+                _STATE["lib"].srt_host_free(_STATE["ctx"], ctypes.c_void_p(self.ptr))
+        except Exception:  # (interpreter shutdown: the process frees it)
+            pass
+
+
+_STATE["blocks"] = {}      # nbytes -> free pinned allocations (pointers)
+_STATE["blocks_out"] = 0   # allocations lent to live arrays
+_BLOCKS_FREE_MAX = 4
+_BLOCKS_OUT_MAX = 16
+
+
+def image_block(nbytes):
+    """A uint8 array of `nbytes` in pinned host memory of its own, for an output that outlives the call
+    (Scene.render's image maps it: the device copies the frame into it at full PCIe rate and PIL takes
+    it without a copy), or None when _BLOCKS_OUT_MAX such arrays are alive already (the caller then
+    copies out of the shared pinned buffer)."""
+    lib, ctx = context()
+    if _STATE["blocks_out"] >= _BLOCKS_OUT_MAX:
+        return None
+    free = _STATE["blocks"].get(nbytes)
+    if free:
+        ptr = free.pop()
+    else:
+        p = ctypes.c_void_p()
+        N.check(lib, lib.srt_host_alloc(ctx, max(int(nbytes), 8), ctypes.byref(p)))
+        ptr = p.value
+    _STATE["blocks_out"] += 1
+    return np.asarray(_HostBlock(ptr, int(nbytes)))
+
+
+def rgb_image(rgbx, width, height, mapped):
+    """PIL RGB image of 4-byte pixels (R, G, B, 255: PIL's own layout of mode RGB).  `mapped`: the image
+    maps `rgbx` (which it keeps alive; read-only, so PIL copies it before any change), else the pixels
+    are copied into a new image.  Either way the image equals Image.fromarray(rgbx[..., :3], "RGB")."""
+    from PIL import Image
+
+    if mapped:
+        try:
+            im = Image.frombuffer("RGBX", (width, height), rgbx, "raw", "RGBX", 0, 1)
+            core = im.im
+            core.setmode("RGB")
+            img = im._new(core)
+            img.readonly = 1
+            if img.mode == "RGB" and img.size == (width, height):
+                return img
+        except Exception:  # (a Pillow without these internals: the copy below)
+            pass
+    img = Image.new("RGB", (width, height), None)
+    img.frombytes(rgbx, "raw", "RGBX")
+    return img
+
+
 def device_buffer(name, nbytes):
     """A named device allocation of the context, grown on demand (kept across calls)."""
     lib, ctx = context()
@@ -206,7 +279,7 @@ def _default_seed():
 
 
 def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None, want_rgb=True, want_hits=False,
-                 jitter_device=None, mt=False, pinned_u8=False, rgbx=False):
+                 jitter_device=None, mt=False, pinned_u8=False, rgbx=False, prefetch=None, out_u8=None):
     """Scene.render on the device.  `jitter` (spp, 4, H*W) from numpy or None for the device RNG;
     `jitter_device`: the same uniforms already in device memory (numpy_uniforms); `mt=True`: the
     jitter is numpy's global stream generated on the device (the reference's draws, including the
@@ -214,9 +287,13 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
     uint8 image lands in the context's pinned host buffer (a view, valid until the next such call)
     instead of a new array.  Without `want_rgb` the linear RGB is resolved and kept in HBM
     (SRT_RENDER_RGB_LOCAL), as the reference keeps it internal.  `rgbx`: the image as 4-byte pixels
-    (R, G, B, 255; SRT_RENDER_RGBX), srgb8 of shape (rows, W, 4)."""
+    (R, G, B, 255; SRT_RENDER_RGBX), srgb8 of shape (rows, W, 4).  `prefetch` (whole frames with
+    `mt`): the jitter's generation is queued on the GPU (srt_render_prefetch) before the scene is
+    lowered and uploaded, so the two overlap (default on; $SIGHTPY_PREFETCH=0 turns it off).
+    `out_u8`: a host uint8 array of the image's size to write the image into (image_block)."""
     lib, ctx = context()
-    upload(scene)
+    if prefetch is None:
+        prefetch = os.environ.get("SIGHTPY_PREFETCH", "1") != "0"
     cam = scene.camera
     W, H = int(cam.screen_width), int(cam.screen_height)
     rows_arr = None if rows is None else np.ascontiguousarray(rows, dtype=np.int32)
@@ -244,14 +321,22 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
             raise ValueError("mt=True draws the jitter itself")
         state = N.MtState.from_numpy()
         a.mt = ctypes.pointer(state)
+    a.flags = (0 if want_rgb else N.RENDER_RGB_LOCAL) | (N.RENDER_RGBX if rgbx else 0)
+    if mt and prefetch and rows_arr is None and nrows == H:
+        N.check(lib, lib.srt_render_prefetch(ctx, ctypes.byref(cd), ctypes.byref(a)))
+    upload(scene)
     rgb = np.empty((3, npix)) if want_rgb else None
     ch = 4 if rgbx else 3
-    u8 = (pinned_buffer("render_u8", ch * npix) if pinned_u8 else np.empty(ch * npix, dtype=np.uint8)).reshape(npix, ch)
+    if out_u8 is not None:
+        if out_u8.dtype != np.uint8 or out_u8.size != ch * npix or not out_u8.flags.c_contiguous:
+            raise ValueError("out_u8 must be a contiguous uint8 array of %d bytes" % (ch * npix))
+        u8 = out_u8.reshape(npix, ch)
+    else:
+        u8 = (pinned_buffer("render_u8", ch * npix) if pinned_u8 else np.empty(ch * npix, dtype=np.uint8)).reshape(npix, ch)
     hits = np.empty((spp, npix), dtype=np.int32) if want_hits else None
     a.out_rgb = N.ptr(rgb)
     a.out_srgb8 = N.ptr(u8)
     a.out_hit_id = N.ptr(hits)
-    a.flags = (0 if want_rgb else N.RENDER_RGB_LOCAL) | (N.RENDER_RGBX if rgbx else 0)
     st = N.Stats()
     N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), ctypes.byref(st)))
     if state is not None:

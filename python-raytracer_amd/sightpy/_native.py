@@ -235,6 +235,8 @@ SIGNATURES = {
     "srt_memcpy": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64]),
     "srt_synchronize": (ctypes.c_int, [_p]),
     "srt_debug_mt_residue": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int64)]),
+    "srt_debug_prefetch_counts": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "srt_render_prefetch": (ctypes.c_int, [_p, ctypes.POINTER(CameraDesc), ctypes.POINTER(RenderArgs)]),
     "srt_render_finish": (ctypes.c_int, [_p, ctypes.POINTER(Stats)]),
     "srt_stream": (ctypes.c_int, [_p, ctypes.POINTER(_p)]),
     "srt_comm_unique_id": (ctypes.c_int, [_p]),

@@ -92,15 +92,16 @@ class Scene:
                 jitter = self.camera.draw_jitter(samples_per_pixel)
                 self.camera.draw_jitter(1)  # reference draws one more get_ray for sizing (scene.py:81)
             # only the uint8 image leaves the GPU (the linear RGB stays there: 8x fewer PCIe bytes), as
-            # 4-byte pixels -- PIL's layout of an RGB image, taken in by a word copy per pixel
+            # 4-byte pixels -- PIL's layout of an RGB image -- into pinned memory of the image's own,
+            # which the returned image maps (no host copy)
+            blk = B.image_block(4 * W * H)
             out = B.render_scene(self, samples_per_pixel, jitter=jitter, seed=seed, batch_size=batch_size,
-                                 want_rgb=False, mt=(rng == "numpy"), pinned_u8=True, rgbx=True)
+                                 want_rgb=False, mt=(rng == "numpy"), pinned_u8=True, rgbx=True, out_u8=blk)
+            self.last_stats = out.stats
+            print("Render Took", time.time() - t0)
+            return B.rgb_image(out.srgb8, W, H, mapped=blk is not None)
         self.last_stats = out.stats
         print("Render Took", time.time() - t0)
-        if out.srgb8.shape[-1] == 4:
-            img = Image.new("RGB", (W, H))
-            img.frombytes(out.srgb8, "raw", "RGBX")
-            return img
         return Image.fromarray(out.srgb8, "RGB")
 
     def get_distances(self):

@@ -729,3 +729,126 @@ def test_gpu_rgbx_output_is_the_uint8_image_with_opaque_alpha():
     np.random.seed(2)
     img = sc.render(2, rng="numpy-host", seed=1)
     assert img.mode == "RGB" and np.array_equal(np.asarray(img), ref.srgb8)
+
+
+def test_gpu_render_prefetch_is_used_and_changes_nothing():
+    """srt_render_prefetch (render_scene queues the numpy-stream generation before lowering and
+    uploading the scene): frames rendered after a prefetch equal frames without one bit for bit, with
+    numpy's state advanced alike; a prefetch the next render does not match -- another spp, a host
+    draw or a device stream draw in between, an option change -- is dropped, and one for a frame of
+    another scene of the same shape is used (the jitter depends only on the stream)."""
+    import ctypes
+    from sightpy import _native as N
+
+    B = _backend()
+    lib, ctx = B.context()
+
+    def counts():
+        u, q = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(lib, lib.srt_debug_prefetch_counts(ctx, ctypes.byref(u), ctypes.byref(q)))
+        return u.value, q.value
+
+    def render(scene, spp, prefetch):
+        out = B.render_scene(scene, spp, mt=True, prefetch=prefetch)
+        return out.rgb.copy(), out.srgb8.copy(), np.random.get_state()
+
+    def same(x, y):
+        assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1])
+        assert np.array_equal(x[2][1], y[2][1]) and x[2][2] == y[2][2]
+
+    def prefetch_only(scene, spp):
+        cd = B.camera_desc(scene.camera)
+        a = N.RenderArgs()
+        a.spp, a.sample_base, a.n_rows, a.batch_spp = spp, 0, int(scene.camera.screen_height), 0
+        a.rows, a.jitter, a.out_hit_id, a.out_rgb, a.out_srgb8, a.seed = None, None, None, None, None, 1
+        st = N.MtState.from_numpy()
+        a.mt = ctypes.pointer(st)
+        N.check(lib, lib.srt_render_prefetch(ctx, ctypes.byref(cd), ctypes.byref(a)))
+
+    sc = scenes.example1(320, 180, 3)
+    sc2 = scenes.example2(320, 180, 3)
+    for spp in (1, 3):
+        np.random.seed(5)
+        ref = render(sc, spp, False)
+        u0, q0 = counts()
+        np.random.seed(5)
+        got = render(sc, spp, True)
+        assert counts() == (u0 + 1, q0 + 1)
+        same(got, ref)
+    # dropped: another spp
+    np.random.seed(7)
+    ref = render(sc, 2, False)
+    u0, _ = counts()
+    np.random.seed(7)
+    prefetch_only(sc, 3)
+    same(render(sc, 2, False), ref)
+    assert counts()[0] == u0
+    # dropped: a host draw, then a device draw of numpy's stream in between
+    np.random.seed(8)
+    np.random.rand(3)
+    ref = render(sc, 2, False)
+    np.random.seed(8)
+    prefetch_only(sc, 2)
+    np.random.rand(3)
+    same(render(sc, 2, False), ref)
+    np.random.seed(9)
+    B.numpy_uniforms(1000)
+    ref = render(sc, 2, False)
+    np.random.seed(9)
+    prefetch_only(sc, 2)
+    B.numpy_uniforms(1000)
+    same(render(sc, 2, False), ref)
+    assert counts()[0] == u0
+    # dropped: an option set in between
+    np.random.seed(10)
+    ref = render(sc, 2, False)
+    np.random.seed(10)
+    prefetch_only(sc, 2)
+    N.check(lib, lib.srt_set_option(ctx, b"mt_short", 65536))
+    same(render(sc, 2, False), ref)
+    assert counts()[0] == u0
+    # used: another scene (lowered and uploaded after the prefetch) of the same frame shape
+    np.random.seed(11)
+    ref2 = render(sc2, 2, False)
+    np.random.seed(11)
+    prefetch_only(sc2, 2)
+    B.upload(sc)
+    got2 = render(sc2, 2, False)  # (uploads sc2 again after the prefetch)
+    assert counts()[0] == u0 + 1
+    same(got2, ref2)
+
+
+def test_gpu_scene_render_images_own_their_pixels():
+    """Scene.render's image maps pinned memory of its own (image_block): a later render does not
+    change an earlier image, a change to an image does not reach another one, the images equal the
+    reference's fromarray of the uint8 frame, and past the pool's cap of live images the pixels are
+    copied instead (same images)."""
+    import gc
+
+    B = _backend()
+    sc = scenes.example1(160, 90, 3)
+    np.random.seed(3)
+    jit = sc.camera.draw_jitter(2)
+    ref = B.render_scene(sc, 2, jitter=jit, seed=1).srgb8
+    np.random.seed(3)
+    a = sc.render(2)
+    a_px = np.asarray(a).copy()
+    assert np.array_equal(a_px, ref)
+    np.random.seed(4)
+    b = sc.render(2)
+    assert np.array_equal(np.asarray(a), a_px) and not np.array_equal(np.asarray(b), a_px)
+    a.putpixel((0, 0), (1, 2, 3))
+    np.random.seed(3)
+    c = sc.render(2)
+    assert np.array_equal(np.asarray(c), a_px) and a.getpixel((0, 0)) == (1, 2, 3)
+    imgs = []
+    for _ in range(B._BLOCKS_OUT_MAX + 4):
+        np.random.seed(3)
+        imgs.append(sc.render(2))
+    assert B._STATE["blocks_out"] <= B._BLOCKS_OUT_MAX
+    for im in imgs:
+        assert im.mode == "RGB" and np.array_equal(np.asarray(im), a_px)
+    del imgs, a, b, c
+    gc.collect()
+    assert B._STATE["blocks_out"] == 0
+    assert sum(len(v) for v in B._STATE["blocks"].values()) <= B._BLOCKS_FREE_MAX

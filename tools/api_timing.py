@@ -59,8 +59,8 @@ def main():
     phases = None
     if a.phases:
         # the same call in its steps (scene.py render): lowering alone, lowering + signature check, the
-        # device frame (render_scene: its own lowering, RGBX image to pinned memory), the PIL image
-        from PIL import Image
+        # device frame (render_scene: its own lowering, RGBX image into the image's pinned block), the
+        # PIL image over that block
         from sightpy import _backend as B
 
         acc = {"lower_only": [], "lower_upload": [], "device_frame": [], "pil": []}
@@ -71,11 +71,12 @@ def main():
             t0 = time.perf_counter()
             B.upload(sc)
             t1 = time.perf_counter()
-            out = B.render_scene(sc, spp, want_rgb=False, mt=True, pinned_u8=True, rgbx=True)
+            blk = B.image_block(4 * W * H)
+            out = B.render_scene(sc, spp, want_rgb=False, mt=True, pinned_u8=True, rgbx=True, out_u8=blk)
             t2 = time.perf_counter()
-            im = Image.new("RGB", (W, H))
-            im.frombytes(out.srgb8, "raw", "RGBX")
+            im = B.rgb_image(out.srgb8, W, H, mapped=blk is not None)
             t3 = time.perf_counter()
+            del im, out, blk
             for k, v in zip(acc, (t0 - tl, t1 - t0, t2 - t1, t3 - t2)):
                 acc[k].append(v)
         phases = {k: round(float(np.median(v)) * 1e3, 3) for k, v in acc.items()}
