@@ -1111,6 +1111,9 @@ constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (regi
 #ifndef RT_FUSE_OCC
 #define RT_FUSE_OCC 3  // waves/SIMD of the fused k_primary (168 VGPRs; its spills: DESIGN.md §3)
 #endif
+#ifndef RT_MESH_FUSE_OCC
+#define RT_MESH_FUSE_OCC RT_FUSE_OCC  // the glossy BVH variant's fused k_primary
+#endif
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
      k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>},
@@ -1121,7 +1124,7 @@ const Variant VARIANTS[] = {
     // a glossy TriangleMesh in the ex1 setting (the mesh bench): the BVH traversal, no other features
     {MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>,
      k_frame<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC, true>,
-     k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, RT_FUSE_OCC, true>},
+     k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, RT_MESH_FUSE_OCC, true>},
     {MAT_GENERIC, k_primary<MAT_GENERIC, OCC>, k_trace<MAT_GENERIC, OCC>, k_frame<MAT_GENERIC, OCC>,
      k_trace<MAT_GENERIC, OCC, true>},
     // scenes with a triangle BVH (TriangleMesh)
