@@ -162,16 +162,17 @@ class _HostBlock:
     def __del__(self):
         try:
             _STATE["blocks_out"] -= 1
-            free = _STATE["blocks"].setdefault(self.nbytes, [])
-            if len(free) < _BLOCKS_FREE_MAX and _STATE["ctx"] is not None:
-                free.append(self.ptr)
-            elif _STATE["ctx"] is not None:
+            if _STATE["ctx"] is None:
+                return
+            if sum(len(v) for v in _STATE["blocks"].values()) < _BLOCKS_FREE_MAX:
+                _STATE["blocks"].setdefault(self.nbytes, []).append(self.ptr)
+            else:
                 _STATE["lib"].srt_host_free(_STATE["ctx"], ctypes.c_void_p(self.ptr))
         except Exception:  # (interpreter shutdown: the process frees it)
             pass
 
 
-_STATE["blocks"] = {}      # nbytes -> free pinned allocations (pointers)
+_STATE["blocks"] = {}      # nbytes -> free pinned allocations (pointers), _BLOCKS_FREE_MAX in all
 _STATE["blocks_out"] = 0   # allocations lent to live arrays
 _BLOCKS_FREE_MAX = 4
 _BLOCKS_OUT_MAX = 16
