@@ -1682,6 +1682,7 @@ struct srt_ctx {
     // the whole frame's uint8 image (host copy of W x H x 3 bytes), as a sharded rank 0 does after the
     // RCCL gather (the transfers themselves are not rehearsed)
     int rehearse_assemble = 0;
+    int sync_blocks = 0;  // option "sync_blocks": k_primary's grid cap in synchronous frames (0: one block per 256 threads)
     double* red = nullptr;      // srt_comm_allreduce scratch
     // srt_render_prefetch: the numpy-stream generation of the synchronous whole frame srt_render is
     // about to be called for, queued before the caller lowers and uploads its scene (Scene.render);
@@ -2523,6 +2524,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     }
     if (!strcmp(key, "collider_seq")) { c->seq_on = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_short_all")) { c->mt_short_all = value != 0; return SRT_OK; }
+    if (!strcmp(key, "sync_blocks")) {
+        if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "sync_blocks: 0 (one block per 256 threads) or a grid cap");
+        c->sync_blocks = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "rehearse_assemble")) {
         if (value != 0 && (value < 2 || value > MAX_RANKS)) return fail(SRT_ERR_ARG, "rehearse_assemble: 0 or 2 .. 64");
         c->rehearse_assemble = (int)value;
@@ -3310,8 +3316,15 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             P.out_u8 = res_u8;
             P.spp_total = a->spp;
             if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
+            // grid: frames in flight overlap one frame's tail with the next, and fewer, longer blocks
+            // (grid-stride, max_blocks: four rounds of the resident blocks) leave the numpy-stream
+            // generators of the frames behind more room; a synchronous frame has nothing to overlap,
+            // so it takes one block per 256 threads and the hardware fills the tail as blocks finish
+            // (same box, ex1 1080p: the synchronous launch 0.950 -> 0.908 ms; pipelined frames with the
+            // full grid 0.902 -> 0.986 ms, profiles/r05_primary_grid_ab.txt)
+            const int pgrid = async ? c->max_blocks : (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX);
             hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
-                               dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, c->max_blocks)), dim3(BLOCK),
+                               dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, pgrid)), dim3(BLOCK),
                                lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ev[1], c->f->stream));
