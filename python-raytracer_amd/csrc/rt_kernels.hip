@@ -638,129 +638,25 @@ __device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3]
 // is traced in the thread too (no ray queues), and a single-pass frame resolves the pixel here
 // (P.fuse_resolve: average, sRGB, uint8; no framebuffer at all).  Otherwise the children are appended
 // to the depth-1 queue for k_trace.
-// (experiments) RT_PRIMARY_VGPR_CAP = k: k_primary allocates at most 2k VGPRs (amdgpu_num_vgpr counts
-// half the unified VGPR+AGPR file on gfx950), e.g. 80 -> 160: 3 waves/SIMD leave 32 registers per SIMD
-// free, room for one small wave of another kernel (the numpy-stream generator) beside them
-#ifdef RT_PRIMARY_VGPR_CAP
-#define RT_PRIMARY_ATTR __attribute__((amdgpu_num_vgpr(RT_PRIMARY_VGPR_CAP)))
-#else
-#define RT_PRIMARY_ATTR
-#endif
 template <uint32_t MATS, int OCC = 2, bool FUSE = false>
-__global__ __launch_bounds__(BLOCK, OCC) RT_PRIMARY_ATTR void k_primary(TraceParams P0) {
-    const TraceParams& P = P0;  // (read in place from the kernel arguments)
-    stage_luts(P);
-    const uint32_t shard = blockIdx.x % NSHARD;
-    uint32_t err = 0;
-    uint32_t shadow = 0;
-    const bool fx = P.fbx != nullptr;
-    const int ppw = 64 / P.pix_groups;  // pixels per wave
-    const int lane = threadIdx.x & 63;
-    const int grp = lane / ppw;
-    const int spg = (P.spp + P.pix_groups - 1) / P.pix_groups;
-    const int s_begin = min(P.spp, grp * spg), s_end = min(P.spp, s_begin + spg);
-    const int64_t nwaves = (P.npix + ppw - 1) / ppw;
-    const Quot qw((double)P.cam.width), qh((double)P.cam.height);
-    for (int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); wv < nwaves;
-         wv += (int64_t)gridDim.x * (BLOCK / 64)) {
-        const int64_t p0 = wv * ppw;
-        const uint32_t p = (uint32_t)(p0 + (lane & (ppw - 1)));
-        const bool pact = p < (uint64_t)P.npix;
-        const bool active = pact && s_begin < s_end;
-        const uint32_t lr = pact ? p / (uint32_t)P.cam.width : 0u;
-        const uint32_t col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
-        const int grow = pact ? P.rows[lr] : 0;
-        const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
-        const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
-        const int s_stop = active ? s_end : s_begin;  // (no samples for a lane past the frame's end)
-        PixAcc acc;
-        // software pipeline: the next sample's pixel jitter is loaded while this sample is traced
-        // (the lens-disk pair of a thin-lens camera is loaded when used: two fewer doubles live
-        // across the trace for the pinhole cameras of every example)
-        double jn[2] = {0.0, 0.0};
-        if (active) primary_jitter(P, s_begin, p, gpix, jn);
-        for (int s = s_begin; s < s_stop; ++s) {
-            Ray r;
-            r.o = r.d = d3{0.0, 0.0, 0.0};
-            r.w = d3{1.0, 1.0, 1.0};
-            r.meta = pack_meta(0, 0, 0);
-            r.pix = p;
-            r.path = mix32(0x5EED0000u, (uint32_t)(P.sample_base + s));
-            double j[4] = {jn[0], jn[1], 0.0, 0.0};
-            RT_T0(tr0);
-            if (P.cam.lens_radius != 0.0) lens_jitter(P, s, p, gpix, j);
-            if (s + 1 < s_stop) primary_jitter(P, s + 1, p, gpix, jn);
-            primary_ray(P.cam, qw, qh, xc, yr, j, r.o, r.d);
-            RT_ACC(0, tr0);
-            int32_t* hs = P.hit_out ? P.hit_out + (int64_t)s * P.npix + p : nullptr;
-            RT_T0(tt0);
-            if (!FUSE) {
-                trace_one<MATS>(P, r, true, err, hs, GpuEmit{P, r, shard, 0u, &shadow, &acc});
-            } else {
-                // the sample's whole path in this thread (single-child scenes): no queue, every
-                // depth's colour into `acc`; the lanes of an iteration share a depth, counted per
-                // wave into the shard's counter of that depth as the queue appends would have been
-                // (the child is written over r: shading reads nothing of the ray after it)
-                // (one loop over the depths, depth 0 included: one inlined copy of the shaders)
-                bool live = true;
-                for (int d = 0;; ++d) {
-                    bool has = false;
-                    trace_one<MATS>(P, r, live, err, d == 0 ? hs : nullptr, FusedEmit{P, r, 0u, &shadow, &acc, &r, &has});
-                    live = live && has;
-                    const uint64_t m = __ballot(live);
-                    if (m == 0) break;
-                    if (live && lanes_below(m) == 0 && d + 1 < SRT_MAX_DEPTHS)  // the lowest live lane
-                        atomicAdd(P.cnt_out + (int64_t)d * NSHARD + shard, (uint32_t)__builtin_popcountll(m));
-                    if (d + 1 > P.dcap) break;  // counted (the host reports rays beyond the cap), not traced
-                }
-            }
-            RT_ACC(3, tt0);
-        }
-        // the pixel's sample groups (lanes of this wave) summed; lane of group 0 stores the pixel
-        PixAcc& acc_r = acc;
-        acc_r.reduce_lanes(fx, ppw);
-        const bool owner = pact && grp == 0;
-        if (FUSE && P.fuse_resolve) {
-            // the frame's only pass: the pixel is complete (scene.py:118-140, k_resolve's rule)
-            uint8_t px[3] = {0, 0, 0};
-            if (owner) {
-                if (fx && acc_r.suspect()) atomicOr(&P.flags[1], RETRY_FIXED_RANGE);
-                const double spp = (double)P.spp_total;
-                const double rr = acc_r.value(fx, 0) / spp, gg = acc_r.value(fx, 1) / spp, bb = acc_r.value(fx, 2) / spp;
-                double a0, a1, a2;
-                resolve_pixel(rr, gg, bb, a0, a1, a2, px);
-                if (P.out_rgb) {
-                    P.out_rgb[p] = rr;
-                    P.out_rgb[P.npix + p] = gg;
-                    P.out_rgb[2 * P.npix + p] = bb;
-                }
-            }
-            if (P.out_u8) store_u8_chunk(P.out_u8 + 3 * p0, px, lane, (int)min<int64_t>(ppw, P.npix - p0));
-        } else if (owner && fx) {
-            // the frame's fixed-point sums (k_trace adds the deeper depths of the per-depth path);
-            // no other thread of this launch touches the pixel
-            float* mg = fx_mag(P.fbx, P.npix) + p;
-            if (P.fb_first) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] = acc_r.w[k];
-                *mg = acc_r.mag;
-            } else {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) P.fbx[k * P.npix + p] += acc_r.w[k];
-                *mg += acc_r.mag;
-            }
-        } else if (owner) {
-            if (P.fb_first) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] = acc_r.value(false, k);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) P.fb[k * P.npix + p] += acc_r.value(false, k);
-            }
-        }
-    }
-    if (err) atomicOr(&P.flags[0], err);
-    if (shadow) atomicAdd(P.shadow, (unsigned long long)shadow);
+__global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
+    constexpr bool LEAN = false;
+#include "rt_primary_body.inc"
+}
+
+// The lean form of the fused paths of single-child scenes without a BVH, for pipelined frames (the
+// headline's kernel; a synchronous frame has no generation beside it and takes k_primary<.., true>):
+// built to 160 VGPRs instead of the 168 of 3 waves/SIMD (amdgpu_num_vgpr counts half the unified
+// VGPR+AGPR file on gfx950), so three trace waves leave 32 registers per SIMD -- room for one
+// four-wave generator workgroup of the next frames' numpy stream (mt_gen_nt: 256 threads, one wave per
+// SIMD) beside them instead of it waiting for a trace wave to end -- and reading the camera coordinates
+// and jitter per sample (LEAN), which holds its spills to the 168-VGPR build's.  Same box, ex1 1080p d5
+// 6 spp pipelined frames 0.901 -> 0.876 ms; the kernel alone (device-resident frames) 0.752 -> 0.762
+// (profiles/r05_lean_primary_ab.txt).
+template <uint32_t MATS, int OCC>
+__global__ __launch_bounds__(BLOCK, OCC) __attribute__((amdgpu_num_vgpr(80))) void k_primary_lean(TraceParams P0) {
+    constexpr bool FUSE = true, LEAN = true;
+#include "rt_primary_body.inc"
 }
 
 // Depth d >= 1: blocks b, b + NSHARD, ... drain input shard b % NSHARD and append to output shard
@@ -1090,6 +986,9 @@ struct Variant {
     void (*frame)(TraceParams);
     void (*chain)(TraceParams);
     void (*fused)(TraceParams) = nullptr;  // k_primary<.., FUSE>: whole single-child paths per pixel
+    // k_primary_lean (160 VGPRs): the fused paths of pipelined frames, whose numpy-stream generators
+    // then run beside them (mt_gen_launch); synchronous frames take `fused`
+    void (*lean)(TraceParams) = nullptr;
 };
 // occupancy experiments for the headline scene (srt_set_option "occupancy" = k in 2..4 selects the
 // build for k waves/SIMD, OCC_VARIANTS[k - 2]; built with -DRT_OCC_VARIANTS); the default
@@ -1116,7 +1015,7 @@ constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (regi
 #endif
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
-     k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>},
+     k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>, k_primary_lean<MATS_GLOSSY_SKY, RT_FUSE_OCC>},
 #ifndef RT_EXP_MIN  // (register-usage experiments, tools/resource_usage.py: the headline variants only, a quicker compile)
     {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
@@ -1150,7 +1049,7 @@ constexpr uint32_t seq_bits(std::initializer_list<int> t) {
 constexpr uint32_t MATS_SEQ_SSPC = MATS_GLOSSY_SKY | seq_bits({SRT_SPHERE, SRT_SPHERE, SRT_PLANE, SRT_CUBOID});
 const Variant SEQ_VARIANTS[] = {
     {MATS_SEQ_SSPC, k_primary<MATS_SEQ_SSPC, OCC>, k_trace<MATS_SEQ_SSPC, OCC>, k_frame<MATS_SEQ_SSPC, OCC>,
-     k_trace<MATS_SEQ_SSPC, OCC, true>, k_primary<MATS_SEQ_SSPC, RT_FUSE_OCC, true>},
+     k_trace<MATS_SEQ_SSPC, OCC, true>, k_primary<MATS_SEQ_SSPC, RT_FUSE_OCC, true>, k_primary_lean<MATS_SEQ_SSPC, RT_FUSE_OCC>},
 };
 #endif
 const Variant& pick_variant(uint32_t mats, uint32_t seq = 0) {
@@ -1683,6 +1582,10 @@ struct srt_ctx {
     // RCCL gather (the transfers themselves are not rehearsed)
     int rehearse_assemble = 0;
     int sync_blocks = 0;  // option "sync_blocks": k_primary's grid cap in synchronous frames (0: one block per 256 threads)
+    // generator workgroup size of the current generation (mt_gen_launch): 256 for the pipelined frames
+    // of a lean k_primary, else MT_GEN_THREADS; option "mt_gen_nt" (0 auto, 256 or 320) forces one
+    int gen_nt = rtmt_dev::MT_GEN_THREADS;
+    int mt_gen_nt_opt = 0;
     double* red = nullptr;      // srt_comm_allreduce scratch
     // srt_render_prefetch: the numpy-stream generation of the synchronous whole frame srt_render is
     // about to be called for, queued before the caller lowers and uploads its scene (Scene.render);
@@ -1986,6 +1889,15 @@ int mt_end_poly_for(srt_ctx* c, int64_t n_words, const uint32_t** out) {
     return SRT_OK;
 }
 
+// The generators of `nseg` segments, one workgroup each: five waves, or four (one per SIMD) for the
+// frames of a lean k_primary (srt_ctx::gen_nt), which leaves room for exactly that beside its waves
+void mt_gen_launch(srt_ctx* c, const MtArgs& G, int nseg, hipStream_t st, uint32_t* win) {
+    if (c->gen_nt == 256)
+        hipLaunchKernelGGL(k_mt_gen<256>, dim3(nseg), dim3(256), 0, st, G, win);
+    else
+        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(nseg), dim3(MT_GEN_THREADS), 0, st, G, win);
+}
+
 // Band mode table of one pass shape: the rows' runs of `ns` samples' stored planes, each segment
 // with its jump polynomial x^(2 d0 - 1) mod phi (xpow_mod, ~2.5 ms each, over a few host threads).
 // Regular runs (a shard's 8-row bands: equal length, equal spacing) with short gaps are merged while
@@ -2129,7 +2041,7 @@ int mt_launch_bands(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* k
     } else {
         gst = st;
     }
-    hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(T.nseg), dim3(MT_GEN_THREADS), 0, gst, G, win);
+    mt_gen_launch(c, G, T.nseg, gst, win);
     HIP_TRY(hipGetLastError());
     if (gen_on) *gen_on = gst;
     c->mt_dirty = false;
@@ -2207,7 +2119,7 @@ int mt_launch(srt_ctx* c, hipStream_t st, uint32_t* win, const uint32_t* key, in
             HIP_TRY(hipStreamWaitEvent(gst, jumped, 0));
             g = gst;
         }
-        hipLaunchKernelGGL(k_mt_gen<MT_GEN_THREADS>, dim3(R.nseg), dim3(MT_GEN_THREADS), 0, g, G, win);
+        mt_gen_launch(c, G, R.nseg, g, win);
         HIP_TRY(hipGetLastError());
         if (gen_on) *gen_on = g;
         c->mt_dirty = false;
@@ -2524,6 +2436,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     }
     if (!strcmp(key, "collider_seq")) { c->seq_on = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_short_all")) { c->mt_short_all = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_gen_nt")) {
+        if (value != 0 && value != 256 && value != 320) return fail(SRT_ERR_ARG, "mt_gen_nt: 0 (auto), 256 or 320");
+        c->mt_gen_nt_opt = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "sync_blocks")) {
         if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "sync_blocks: 0 (one block per 256 threads) or a grid cap");
         c->sync_blocks = (int)value;
@@ -3111,6 +3028,10 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
     srt_stats S{};
     // this frame's first-pass generation already queued by srt_render_prefetch (same stream state,
     // same frame shape, nothing generated since): not launched again (the first iteration only)
+    // generator width: four waves (one per SIMD) beside the lean fused kernel of the frames in flight
+    c->gen_nt = c->mt_gen_nt_opt ? c->mt_gen_nt_opt
+                                 : ((async && F.fuse && pick_variant(c->mats, c->seq_on ? c->seq : 0).lean != nullptr) ? 256
+                                                                                                          : rtmt_dev::MT_GEN_THREADS);
     bool pf_hit = false;
     const int mts = use_mt ? (c->use_mt_stream >= 0 ? c->use_mt_stream : (n_rows >= Hf ? 2 : 0)) : 0;
     const int64_t pf_shape[8] = {W, Hf, a->spp, batch, mt_pm, (int64_t)(c->f - c->slots), mts,
@@ -3323,7 +3244,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             // (same box, ex1 1080p: the synchronous launch 0.950 -> 0.908 ms; pipelined frames with the
             // full grid 0.902 -> 0.986 ms, profiles/r05_primary_grid_ab.txt)
             const int pgrid = async ? c->max_blocks : (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX);
-            hipLaunchKernelGGL(F.fuse ? V.fused : V.primary,
+            hipLaunchKernelGGL(F.fuse ? ((async && V.lean) ? V.lean : V.fused) : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, pgrid)), dim3(BLOCK),
                                lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());

@@ -233,3 +233,52 @@ def test_short_segment_frames_equal_tabulated_segment_frames():
         N.check(lib, lib.srt_set_option(ctx, b"mt_short", 65536))
     assert np.array_equal(a.rgb, b.rgb) and np.array_equal(a.srgb8, b.srgb8)
     assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
+
+
+@pytest.mark.gpu
+def test_generator_width_gives_the_same_frames():
+    """Pipelined frames of the lean fused kernel generate numpy's stream with four-wave generator
+    workgroups (one wave per SIMD beside the trace waves; option mt_gen_nt auto = 256), other frames with
+    five-wave ones: both widths give the same images and numpy state, whole frames and a shard's rows."""
+    import ctypes
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    sc = scenes.example1(640, 360, 3)
+    rows = [r for r in range(360) if (r // 9) % 8 == 3]
+
+    def frames():
+        np.random.seed(23)
+        cd = B.camera_desc(sc.camera)
+        out = []
+        for rr in (None, rows):
+            a = N.RenderArgs()
+            n = 360 if rr is None else len(rr)
+            ra = None if rr is None else np.ascontiguousarray(rr, dtype=np.int32)
+            a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, n, 0
+            a.rows, a.jitter, a.out_hit_id, a.out_rgb, a.seed = N.ptr(ra), None, None, None, 1
+            mt = N.MtState.from_numpy()
+            a.mt = ctypes.pointer(mt)
+            a.flags = N.RENDER_ASYNC
+            bufs = [B.pinned_buffer("width_u8_%d_%d" % (n, k), 3 * 640 * n) for k in range(3)]
+            for k in range(3):
+                a.out_srgb8 = N.ptr(bufs[k])
+                N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+            N.check(lib, lib.srt_render_finish(ctx, None))
+            mt.to_numpy()
+            out += [b.copy() for b in bufs]
+        return out, np.random.get_state()
+
+    try:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_gen_nt", 0))
+        auto, sa = frames()
+        N.check(lib, lib.srt_set_option(ctx, b"mt_gen_nt", 320))
+        five, sb = frames()
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_gen_nt", 0))
+    for x, y in zip(auto, five):
+        assert np.array_equal(x, y)
+    assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
+    assert lib.srt_set_option(ctx, b"mt_gen_nt", 100) != 0
