@@ -1582,6 +1582,7 @@ struct srt_ctx {
     // RCCL gather (the transfers themselves are not rehearsed)
     int rehearse_assemble = 0;
     int sync_blocks = 0;  // option "sync_blocks": k_primary's grid cap in synchronous frames (0: one block per 256 threads)
+    int lean_blocks = 0;  // option "lean_blocks": grid of k_primary_lean in pipelined frames (0: max_blocks; set to 2 per CU)
     // generator workgroup size of the current generation (mt_gen_launch): 256 for the pipelined frames
     // of a lean k_primary, else MT_GEN_THREADS; option "mt_gen_nt" (0 auto, 256 or 320) forces one
     int gen_nt = rtmt_dev::MT_GEN_THREADS;
@@ -2388,6 +2389,7 @@ int srt_create(int device, srt_ctx** out) {
     // (the frame kernel) per slot, or four rounds of the OCC resident 256-thread blocks of the
     // grid-stride kernels
     c->max_blocks = prop.multiProcessorCount * 4 * OCC;
+    c->lean_blocks = prop.multiProcessorCount * 2;
     int rc = ensure_slot(c->slots[0]);
     if (rc) {
         delete c;
@@ -2439,6 +2441,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!strcmp(key, "mt_gen_nt")) {
         if (value != 0 && value != 256 && value != 320) return fail(SRT_ERR_ARG, "mt_gen_nt: 0 (auto), 256 or 320");
         c->mt_gen_nt_opt = (int)value;
+        return SRT_OK;
+    }
+    if (!strcmp(key, "lean_blocks")) {
+        if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "lean_blocks: 0 (max_blocks) or a grid size");
+        c->lean_blocks = (int)value;
         return SRT_OK;
     }
     if (!strcmp(key, "sync_blocks")) {
@@ -3243,8 +3250,15 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             // so it takes one block per 256 threads and the hardware fills the tail as blocks finish
             // (same box, ex1 1080p: the synchronous launch 0.950 -> 0.908 ms; pipelined frames with the
             // full grid 0.902 -> 0.986 ms, profiles/r05_primary_grid_ab.txt)
-            const int pgrid = async ? c->max_blocks : (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX);
-            hipLaunchKernelGGL(F.fuse ? ((async && V.lean) ? V.lean : V.fused) : V.primary,
+            // the lean kernel of pipelined whole frames (its generators beside it): two blocks per CU,
+            // each grid-striding over ~30 wave iterations of a 1080p frame; the frames in flight fill
+            // the rest of the CU (ex1 1080p: 0.878 ms per frame at 3072 blocks, 0.838 at 512; a rank of
+            // 8's shard, 2025 blocks at most, was slower with it: profiles/r05_lean_grid_ab.txt; option
+            // lean_blocks)
+            const bool lean = F.fuse && async && V.lean;
+            const int pgrid = !async ? (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX)
+                                     : (lean && n_rows == Hf && c->lean_blocks > 0 ? c->lean_blocks : c->max_blocks);
+            hipLaunchKernelGGL(F.fuse ? (lean ? V.lean : V.fused) : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, pgrid)), dim3(BLOCK),
                                lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
