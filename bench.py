@@ -263,7 +263,7 @@ def roofline(kname, kms, model_bytes, path, krec, src):
     if krec.get("wave_wait_frac") is not None:
         roof["wave_wait_frac"] = round(krec["wave_wait_frac"], 4)
     if "valu_issue_frac" in roof and "wave_wait_frac" in roof:
-        roof["limiter"] = ("latency: 3 waves/SIMD (168 VGPRs); waves wait on memory %.0f%% of their cycles, VALU "
+        roof["limiter"] = ("latency: 3 waves/SIMD; waves wait on memory %.0f%% of their cycles, VALU "
                            "issue %.0f%% busy, HBM %.0f%% of peak" % (100 * roof["wave_wait_frac"],
                                                                     100 * roof["valu_issue_frac"],
                                                                     100 * roof["traffic_frac"]))
@@ -731,6 +731,23 @@ def main():
             stats.append(s.as_dict())
         sec["frame_latency_ms"] = round(float(np.median(lat)), 4)
         sec["stats"] = stats
+        if stats[0]["kernel_path"] == "fused" and not args.sync:
+            # the pipelined frames' kernel (k_primary_lean, when the scene has one) timed alone in the same
+            # synchronous frames (option sync_lean), for the roofline
+            n0, n1 = ctypes.c_int64(0), ctypes.c_int64(0)
+            N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n0)))
+            N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 1))
+            lean_stats = []
+            try:
+                for _ in range(3):
+                    s = N.Stats()
+                    step(async_ok=False, st=s)
+                    lean_stats.append(s.as_dict())
+            finally:
+                N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 0))
+            N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n1)))
+            if n1.value > n0.value:
+                sec["stats_lean"] = lean_stats
         if world == 1 and rows32 is None:
             # the round-1 headline form: jitter resident in HBM, outputs left in HBM
             nj = spp * 4 * npix_full
@@ -819,8 +836,14 @@ def main():
             # one launch of the dominant kernel: a frame of `passes` passes launches it once per pass
             npass = max(1, st0[0]["passes"])
             kms = float(np.mean([x["ms_primary_kernel"] for x in st0])) / npass
+            kms_sync = None
+            variant = {"fused": ", true>", "primary": ", false>"}.get(path)
+            if "stats_lean" in sec:
+                # the timed region's kernel: the lean form the pipelined frames run
+                kms_sync, kname, variant = kms, "k_primary_lean", None
+                kms = float(np.mean([x["ms_primary_kernel"] for x in sec["stats_lean"]])) / npass
             krec, src = (None, None) if (args.size or args.spp or world > 1 or rows32 is not None) else \
-                pmc_counters(args.config, kname, {"fused": ", true>", "primary": ", false>"}.get(path))
+                pmc_counters(args.config, kname, variant)
             from sightpy._shard import shard_rows
 
             npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0, kmax, snake)) * W
@@ -832,6 +855,11 @@ def main():
                 roof["passes_per_frame"] = npass
             roof["kernel_ms_note"] = ("one launch in a synchronous frame (HIP events); pipelined frames overlap one "
                                       "frame's tail with the next, so ms_per_step can be below it")
+            if kms_sync is not None:
+                roof["kernel_ms_note"] += ("; the kernel the pipelined frames run (k_primary_lean), timed alone in "
+                                           "synchronous frames (option sync_lean)")
+                roof["sync_frames_kernel"] = {"kernel": "k_primary (fused paths: synchronous frames, Scene.render)",
+                                              "kernel_ms": round(kms_sync / 1.0, 4)}
             rec["roofline"] = roof
         if not args.no_cpu_baseline and world == 1 and args.config in CPU_SKIP:
             rec["cpu_baseline"] = {"value": None, "skipped": CPU_SKIP[args.config]}

@@ -410,6 +410,9 @@ int srt_debug_mt_residue(srt_ctx* ctx, int64_t* nonzero_words);
 /* Diagnostic: renders that found their generation queued by srt_render_prefetch (used, not
  * launched again) and prefetches queued, since the context was created. */
 int srt_debug_prefetch_counts(srt_ctx* ctx, int64_t* used, int64_t* queued);
+/* Diagnostic: launches of the lean fused kernel (k_primary_lean: pipelined frames of single-child
+ * scenes without a BVH, or any frame with option "sync_lean") since the context was created. */
+int srt_debug_lean_launches(srt_ctx* ctx, int64_t* launches);
 const char* srt_last_error(void);
 
 #ifdef __cplusplus

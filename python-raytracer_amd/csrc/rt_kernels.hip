@@ -1583,6 +1583,8 @@ struct srt_ctx {
     int rehearse_assemble = 0;
     int sync_blocks = 0;  // option "sync_blocks": k_primary's grid cap in synchronous frames (0: one block per 256 threads)
     int lean_blocks = 0;  // option "lean_blocks": grid of k_primary_lean in pipelined frames (0: max_blocks; set to 2 per CU)
+    bool sync_lean = false;     // option "sync_lean": synchronous frames run k_primary_lean too (measurement)
+    int64_t lean_launches = 0;  // (srt_debug_lean_launches)
     // generator workgroup size of the current generation (mt_gen_launch): 256 for the pipelined frames
     // of a lean k_primary, else MT_GEN_THREADS; option "mt_gen_nt" (0 auto, 256 or 320) forces one
     int gen_nt = rtmt_dev::MT_GEN_THREADS;
@@ -2443,6 +2445,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         c->mt_gen_nt_opt = (int)value;
         return SRT_OK;
     }
+    if (!strcmp(key, "sync_lean")) { c->sync_lean = value != 0; return SRT_OK; }
     if (!strcmp(key, "lean_blocks")) {
         if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "lean_blocks: 0 (max_blocks) or a grid size");
         c->lean_blocks = (int)value;
@@ -3255,7 +3258,10 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             // the rest of the CU (ex1 1080p: 0.878 ms per frame at 3072 blocks, 0.838 at 512; a rank of
             // 8's shard, 2025 blocks at most, was slower with it: profiles/r05_lean_grid_ab.txt; option
             // lean_blocks)
-            const bool lean = F.fuse && async && V.lean;
+            // (option sync_lean: synchronous frames take the lean kernel too -- bench.py times the pipelined
+            // frames' kernel alone that way for its roofline)
+            const bool lean = F.fuse && (async || c->sync_lean) && V.lean;
+            if (lean) c->lean_launches++;
             const int pgrid = !async ? (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX)
                                      : (lean && n_rows == Hf && c->lean_blocks > 0 ? c->lean_blocks : c->max_blocks);
             hipLaunchKernelGGL(F.fuse ? (lean ? V.lean : V.fused) : V.primary,
@@ -4139,6 +4145,12 @@ int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
     return SRT_OK;
 }
 #endif
+
+int srt_debug_lean_launches(srt_ctx* c, int64_t* launches) {
+    if (!c || !launches) return fail(SRT_ERR_ARG, "null argument");
+    *launches = c->lean_launches;
+    return SRT_OK;
+}
 
 int srt_debug_prefetch_counts(srt_ctx* c, int64_t* used, int64_t* queued) {
     if (!c || !used || !queued) return fail(SRT_ERR_ARG, "null argument");
