@@ -1583,6 +1583,9 @@ struct srt_ctx {
     int rehearse_assemble = 0;
     int sync_blocks = 0;  // option "sync_blocks": k_primary's grid cap in synchronous frames (0: one block per 256 threads)
     int lean_blocks = 0;  // option "lean_blocks": grid of k_primary_lean in pipelined frames (0: max_blocks; set to 2 per CU)
+    // option "lean_blocks_shard": the same for a shard's rows (0: max_blocks; set to 4 per CU: every rank of 4
+    // rehearsed, slowest 0.321 -> 0.275 ms per frame; of 8 unchanged, profiles/r05_lean_grid_ab.txt)
+    int lean_blocks_shard = 0;
     bool sync_lean = false;     // option "sync_lean": synchronous frames run k_primary_lean too (measurement)
     int64_t lean_launches = 0;  // (srt_debug_lean_launches)
     // generator workgroup size of the current generation (mt_gen_launch): 256 for the pipelined frames
@@ -2392,6 +2395,7 @@ int srt_create(int device, srt_ctx** out) {
     // grid-stride kernels
     c->max_blocks = prop.multiProcessorCount * 4 * OCC;
     c->lean_blocks = prop.multiProcessorCount * 2;
+    c->lean_blocks_shard = prop.multiProcessorCount * 4;
     int rc = ensure_slot(c->slots[0]);
     if (rc) {
         delete c;
@@ -2446,6 +2450,11 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         return SRT_OK;
     }
     if (!strcmp(key, "sync_lean")) { c->sync_lean = value != 0; return SRT_OK; }
+    if (!strcmp(key, "lean_blocks_shard")) {
+        if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "lean_blocks_shard: 0 (max_blocks) or a grid size");
+        c->lean_blocks_shard = (int)value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "lean_blocks")) {
         if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "lean_blocks: 0 (max_blocks) or a grid size");
         c->lean_blocks = (int)value;
@@ -3257,13 +3266,17 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             // each grid-striding over ~30 wave iterations of a 1080p frame; the frames in flight fill
             // the rest of the CU (ex1 1080p: 0.878 ms per frame at 3072 blocks, 0.838 at 512; a rank of
             // 8's shard, 2025 blocks at most, was slower with it: profiles/r05_lean_grid_ab.txt; option
-            // lean_blocks)
+            // lean_blocks).  A pipeline's first frame, with nothing in flight to fill the CUs around its
+            // blocks, keeps the full four rounds (max_blocks).
             // (option sync_lean: synchronous frames take the lean kernel too -- bench.py times the pipelined
             // frames' kernel alone that way for its roofline)
             const bool lean = F.fuse && (async || c->sync_lean) && V.lean;
             if (lean) c->lean_launches++;
             const int pgrid = !async ? (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX)
-                                     : (lean && n_rows == Hf && c->lean_blocks > 0 ? c->lean_blocks : c->max_blocks);
+                                     : (!lean || c->async_pending == 0               ? c->max_blocks
+                                        : n_rows == Hf && c->lean_blocks > 0              ? c->lean_blocks
+                                        : n_rows < Hf && c->lean_blocks_shard > 0         ? c->lean_blocks_shard
+                                                                                            : c->max_blocks);
             hipLaunchKernelGGL(F.fuse ? (lean ? V.lean : V.fused) : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, pgrid)), dim3(BLOCK),
                                lut_bytes(c), c->f->stream, P);
