@@ -852,3 +852,57 @@ def test_gpu_scene_render_images_own_their_pixels():
     gc.collect()
     assert B._STATE["blocks_out"] == 0
     assert sum(len(v) for v in B._STATE["blocks"].values()) <= B._BLOCKS_FREE_MAX
+
+
+def test_gpu_grid_and_kernel_form_options_give_the_same_frames():
+    """The synchronous launch's grid (sync_blocks: full grid or capped), the lean kernel of pipelined
+    frames and its grid (lean_blocks, lean_blocks_shard) and the lean kernel in synchronous frames
+    (sync_lean) change how the work is spread, not what is summed: the same images, whole frames and
+    a shard's rows, synchronous and pipelined (fixed-point sums are exact in any grouping)."""
+    import ctypes
+    from sightpy import _native as N
+
+    B = _backend()
+    lib, ctx = B.context()
+    sc = scenes.example1(640, 360, 3)
+    rows = np.ascontiguousarray([r for r in range(360) if (r // 9) % 4 == 1], dtype=np.int32)
+    cd = B.camera_desc(sc.camera)
+
+    def frames():
+        outs = []
+        for rr in (None, rows):
+            n = 360 if rr is None else len(rr)
+            np.random.seed(31)
+            jit = np.ascontiguousarray(np.random.rand(2, 4, 640 * n))
+            sync = B.render_scene(sc, 2, jitter=jit, seed=1, rows=rr)
+            outs += [sync.rgb.copy(), sync.srgb8.copy()]
+            jd = B.device_buffer("grid_jit_%d" % n, jit.nbytes)
+            N.check(lib, lib.srt_memcpy(ctx, jd, N.ptr(jit), jit.nbytes))
+            a = N.RenderArgs()
+            a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, n, 0
+            a.rows, a.jitter, a.out_hit_id, a.mt, a.seed = N.ptr(rr), jd, None, None, 1
+            a.flags = N.RENDER_ASYNC
+            bufs = [B.pinned_buffer("grid_u8_%d_%d" % (n, k), 3 * 640 * n) for k in range(3)]
+            for k in range(3):
+                a.out_srgb8 = N.ptr(bufs[k])
+                N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+            N.check(lib, lib.srt_render_finish(ctx, None))
+            outs += [b.copy().reshape(n, 640, 3) for b in bufs]
+        return outs
+
+    def opts(**kv):
+        for k, v in kv.items():
+            N.check(lib, lib.srt_set_option(ctx, k.encode(), v))
+
+    ref = frames()
+    try:
+        for kv in ({"sync_blocks": 3072, "lean_blocks": 0, "lean_blocks_shard": 0},
+                   {"sync_lean": 1, "lean_blocks": 1024, "lean_blocks_shard": 256}):
+            opts(**kv)
+            got = frames()
+            for x, y in zip(ref, got):
+                assert np.array_equal(x, y)
+            opts(sync_blocks=0, lean_blocks=512, lean_blocks_shard=1024, sync_lean=0)
+    finally:
+        opts(sync_blocks=0, lean_blocks=512, lean_blocks_shard=1024, sync_lean=0)
+    assert np.array_equal(ref[2], ref[1]) and np.array_equal(ref[3], ref[1])  # pipelined == synchronous
