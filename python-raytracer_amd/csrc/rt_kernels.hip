@@ -1491,6 +1491,12 @@ struct srt_ctx {
     // option "mt_short_all": pipelined whole frames take the short segments too (their generation's
     // latency, not only the first frame's, then shrinks, for four times the jumps)
     bool mt_short_all = false;
+    // option "mt_pipe_split": doubles per band-mode segment of a pipelined whole frame behind others in
+    // flight (0: the tabulated 2^19-word segments).  Band mode generates exactly the stored planes' runs
+    // (a tabulated segment straddling a stored and a skipped plane generates both), each run cut at the
+    // split: same box, ex1 1080p pipelined frames 0.84 ms tabulated, 0.794 at 2^18 doubles (the
+    // tabulated segments' length), 1.12 at 2^19 (longer generator chains); profiles/r05_pipe_split_ab.txt
+    int64_t mt_pipe_split = (int64_t)1 << 18;
     double* mt_out = nullptr;  // staging for srt_mt19937_uniforms into host memory
     int64_t mt_out_cap = 0;
     // -1 auto: k_frame for scenes whose rays branch (refractive / thin-film / diffuse fan-out),
@@ -2444,6 +2450,12 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     }
     if (!strcmp(key, "collider_seq")) { c->seq_on = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_short_all")) { c->mt_short_all = value != 0; return SRT_OK; }
+    if (!strcmp(key, "mt_pipe_split")) {
+        if (value != 0 && (value < 4096 || value > ((int64_t)1 << 24)))
+            return fail(SRT_ERR_ARG, "mt_pipe_split: 0 or 4096 .. 2^24 doubles");
+        c->mt_pipe_split = value;
+        return SRT_OK;
+    }
     if (!strcmp(key, "mt_gen_nt")) {
         if (value != 0 && value != 256 && value != 320) return fail(SRT_ERR_ARG, "mt_gen_nt: 0 (auto), 256 or 320");
         c->mt_gen_nt_opt = (int)value;
@@ -2889,13 +2901,14 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
         c->mt_end_polys.clear();
     }
     // a whole frame with nothing in flight (synchronous, or the first of a pipeline): short segments in
-    // band mode (srt_ctx::mt_short); later pipelined frames generate behind their predecessors
-    // (tabulated 2^19-word segments, fewer jumps)
-    const bool mt_short = use_mt && c->mt_bands_on && c->mt_short > 0 && n_rows == Hf &&
-                          (c->async_pending == 0 || c->mt_short_all);
-    if (use_mt && c->mt_bands_on && (n_rows < Hf || mt_short)) {
+    // band mode (srt_ctx::mt_short); later pipelined frames generate behind their predecessors in
+    // band-mode segments of mt_pipe_split doubles (0: the tabulated 2^19-word segments)
+    const int64_t whole_split = n_rows < Hf ? 0
+                              : (c->async_pending == 0 || c->mt_short_all) ? c->mt_short
+                                                                           : c->mt_pipe_split;
+    if (use_mt && c->mt_bands_on && (n_rows < Hf || whole_split > 0)) {
         const int last_ns = a->spp - (F.npass - 1) * batch;
-        const int64_t split = n_rows < Hf ? (int64_t)1 << 18 : c->mt_short;
+        const int64_t split = n_rows < Hf ? (int64_t)1 << 18 : whole_split;
         for (int k = 0; k < 2; ++k) {
             if ((rc = mt_band_table(c, W, Hf, k == 0 ? batch : last_ns, mt_pm, rows_src, n_rows, split, &mt_bt[k])))
                 return rc;
