@@ -282,3 +282,50 @@ def test_generator_width_gives_the_same_frames():
         assert np.array_equal(x, y)
     assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
     assert lib.srt_set_option(ctx, b"mt_gen_nt", 100) != 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [0, 65536, 262144])
+def test_pipelined_frames_segment_length_gives_the_same_frames(split):
+    """Pipelined whole frames behind others in flight generate numpy's stream in band-mode segments of
+    mt_pipe_split doubles (0: the tabulated 2^19-word segments): the same images and numpy state for
+    every split, thin-lens camera (all four planes) included."""
+    import ctypes
+
+    import scenes
+    from sightpy import _backend as B, _native as N
+
+    lib, ctx = B.context()
+    sc = scenes.example1(640, 360, 3)
+
+    def frames(lens):
+        sc.camera.lens_radius = lens
+        np.random.seed(41)
+        cd = B.camera_desc(sc.camera)
+        a = N.RenderArgs()
+        a.spp, a.sample_base, a.n_rows, a.batch_spp = 2, 0, 360, 0
+        a.rows, a.jitter, a.out_hit_id, a.out_rgb, a.seed = None, None, None, None, 1
+        mt = N.MtState.from_numpy()
+        a.mt = ctypes.pointer(mt)
+        a.flags = N.RENDER_ASYNC
+        bufs = [B.pinned_buffer("split_u8_%d" % k, 3 * 640 * 360) for k in range(4)]
+        for k in range(4):
+            a.out_srgb8 = N.ptr(bufs[k])
+            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(a), None))
+        N.check(lib, lib.srt_render_finish(ctx, None))
+        mt.to_numpy()
+        return [b.copy() for b in bufs], np.random.get_state()
+
+    lens0 = sc.camera.lens_radius
+    try:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_pipe_split", 0))
+        ref = [frames(0.0), frames(0.05)]
+        N.check(lib, lib.srt_set_option(ctx, b"mt_pipe_split", split))
+        got = [frames(0.0), frames(0.05)]
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"mt_pipe_split", 262144))
+        sc.camera.lens_radius = lens0
+    for (ra, sa), (rb, sb) in zip(ref, got):
+        for x, y in zip(ra, rb):
+            assert np.array_equal(x, y)
+        assert sa[2] == sb[2] and np.array_equal(sa[1], sb[1])
