@@ -37,6 +37,7 @@ struct BvhBuild {
     std::vector<BvhNode> nodes;
     std::vector<int32_t> tri;  // collider index per leaf slot
     std::vector<int32_t> lin;  // colliders outside the BVH, ascending
+    float bound = 0.0f;        // max |coordinate| over the nodes' (non-empty) boxes: rt_device.h box_ray
 };
 
 namespace bvh_detail {
@@ -66,6 +67,7 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
     out.nodes.clear();
     out.tri.clear();
     out.lin.clear();
+    out.bound = 0.0f;
     std::vector<Item> items;
     for (int i = 0; i < n; ++i)
         if (col[i].type == SRT_TRIANGLE) {
@@ -260,6 +262,11 @@ inline void bvh_build(const srt_collider* col, int n, BvhBuild& out) {
             for (int i = 0; i < n; ++i) out.lin.push_back(i);
             return;
         }
+    for (const BvhNode& nd : out.nodes)
+        for (int k = 0; k < 4; ++k)
+            if (nd.child[k] != BVH_EMPTY)
+                for (int a = 0; a < 3; ++a)
+                    out.bound = std::max(out.bound, std::max(std::fabs(nd.lo[a][k]), std::fabs(nd.hi[a][k])));
 }
 
 }  // namespace rt

@@ -270,9 +270,11 @@ struct SceneView {
     const RT_RO int32_t* bvh_tri;  // collider index of each BVH leaf slot
     int bvh_nodes;                 // 0: no BVH
     int sky_col;                   // the one collider shaded by a SkyBox / Panorama material, else -1
+    float bvh_bound;               // max |coordinate| of the BVH's boxes (the f32 box test's error bound)
+    int32_t pad_;
 };
 // the host builds SceneView/TraceParams and the device reads them: the layout must agree
-static_assert(sizeof(SceneView) == 176 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
+static_assert(sizeof(SceneView) == 184 && offsetof(SceneView, nlut_lds) == 136, "SceneView layout");
 
 // BVH node, 4-wide (128 B: one traversal step loads one cache line and tests four boxes): child k's
 // box [lo[.][k], hi[.][k]] in float, rounded outward from the build's f64 boxes (which are inflated so
@@ -651,6 +653,7 @@ RT_HD void primary_ray(const srt_camera& cam, double xc, double yr, const double
 // Ray/box slab test of child k of a 4-wide node (f64 arithmetic on the float bounds): entry
 // distance `tnear`; an axis whose slab product is NaN (an axis-parallel ray exactly on a slab plane)
 // constrains nothing (conservative).
+#ifdef RT_BVH_F64
 RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear) {
     double t0 = -INFINITY, t1 = INFINITY;
     const double o[3] = {O.x, O.y, O.z}, iv[3] = {inv.x, inv.y, inv.z};
@@ -663,6 +666,45 @@ RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear)
     }
     tnear = t0;
     return t0 <= t1 && t1 >= 0.0;
+}
+#endif
+
+// The same slab test in f32 arithmetic (half the registers and VALU cycles of the f64 test above,
+// which the RT_BVH_F64 experiment build keeps), widened so that it never rejects a box the exact
+// test accepts.  Per ray and axis: iv = f32(1/D), noiv = -f32(O/D), so a slab plane's distance is
+// one fma, fma(x, iv, noiv) -- within 2.001 * 2^-24 * |1/D| * (|x| + |O|) of (x - O)/D, x a box bound
+// (|x| <= S.bvh_bound).  Each axis's entry / exit is then moved out by e = 2^-20 |1/D| (bound + |O|),
+// 8x that error bound (and the f32 rounding of the subtraction / addition), so the f32 interval holds
+// the exact one, and `tnear` is a lower bound of the exact entry distance.  An axis whose
+// |1/D| (bound + |O|) is not below 1e37 (an axis-parallel ray: 1/D = inf; NaN) constrains nothing
+// (conservative), which also keeps every product finite.
+#ifndef RT_BOX_MARGIN
+#define RT_BOX_MARGIN 0x1p-20  // (tests/test_mesh.py checks that 0 fails the conservativeness probe)
+#endif
+struct BoxRay {
+    float iv[3], noiv[3], e[3];
+};
+RT_HD BoxRay box_ray(d3 O, d3 inv, float bound) {
+    BoxRay r;
+    const double o[3] = {O.x, O.y, O.z}, iv[3] = {inv.x, inv.y, inv.z};
+    for (int a = 0; a < 3; ++a) {
+        const double s = fabs(iv[a]) * ((double)bound + fabs(o[a]));
+        const bool ok = s < 1e37;
+        r.iv[a] = ok ? (float)iv[a] : 0.0f;
+        r.noiv[a] = ok ? -(float)(o[a] * iv[a]) : 0.0f;
+        r.e[a] = ok ? (float)(RT_BOX_MARGIN * s) : INFINITY;
+    }
+    return r;
+}
+RT_HD bool box4f_hit(const RT_RO BvhNode& nd, int k, const BoxRay& r, float& tnear) {
+    float t0 = -INFINITY, t1 = INFINITY;
+    for (int a = 0; a < 3; ++a) {
+        const float p = fmaf(nd.lo[a][k], r.iv[a], r.noiv[a]), q = fmaf(nd.hi[a][k], r.iv[a], r.noiv[a]);
+        t0 = fmaxf(t0, fminf(p, q) - r.e[a]);
+        t1 = fminf(t1, fmaxf(p, q) + r.e[a]);
+    }
+    tnear = t0;
+    return t0 <= t1 && t1 >= 0.0f;
 }
 
 // Traversal stack entries, one 64-bit word each: the entry distance as float bits (rounded down: a
@@ -692,9 +734,25 @@ RT_HD float bvh_u2f(uint32_t u) {
     return f;
 #endif
 }
-RT_HD uint64_t bvh_entry(double tn, int32_t code) {
+// the box test's distance type and its per-ray operands
+#ifdef RT_BVH_F64
+using bvh_t = double;
+struct BvhRay {
+    d3 O, inv;
+};
+RT_HD BvhRay bvh_ray(const SceneView&, d3 O, d3 D) { return BvhRay{O, d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z}}; }
+#else
+using bvh_t = float;
+struct BvhRay {
+    BoxRay b;
+};
+RT_HD BvhRay bvh_ray(const SceneView& S, d3 O, d3 D) {
+    return BvhRay{box_ray(O, d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z}, S.bvh_bound)};
+}
+#endif
+RT_HD uint64_t bvh_entry(bvh_t tn, int32_t code) {
     float f = (float)tn;
-    if ((double)f > tn) f = nextafterf(f, -INFINITY);
+    if ((double)f > (double)tn) f = nextafterf(f, -INFINITY);
     return ((uint64_t)bvh_f2u(f) << 32) | (uint32_t)code;
 }
 RT_HD int32_t bvh_code(int32_t child, int32_t count) {
@@ -706,18 +764,23 @@ RT_HD int32_t bvh_code(int32_t child, int32_t count) {
 
 // The four children of a node against the ray: entry distances t[k] (INFINITY: missed, empty, or
 // entered beyond `limit`) and child codes c[k], sorted by distance (a sorting network on registers).
-RT_HD void bvh_children(const RT_RO BvhNode& nd, d3 O, d3 inv, double limit, bool strict, double t[4],
+RT_HD void bvh_children(const RT_RO BvhNode& nd, const BvhRay& R, double limit, bool strict, bvh_t t[4],
                         int32_t c[4]) {
 RT_UNROLL
     for (int k = 0; k < 4; ++k) {
         c[k] = bvh_code(nd.child[k], nd.count[k]);  // (an empty slot's code is never used: t = INFINITY)
-        double tn;
-        const bool hit = nd.child[k] != BVH_EMPTY && box4_hit(nd, k, O, inv, tn) && (strict ? tn < limit : tn <= limit);
-        t[k] = hit ? tn : INFINITY;
+        bvh_t tn;
+#ifdef RT_BVH_F64
+        const bool box = box4_hit(nd, k, R.O, R.inv, tn);
+#else
+        const bool box = box4f_hit(nd, k, R.b, tn);
+#endif
+        const bool hit = nd.child[k] != BVH_EMPTY && box && (strict ? (double)tn < limit : (double)tn <= limit);
+        t[k] = hit ? tn : (bvh_t)INFINITY;
     }
     auto cs = [&](int a, int b) {
         const bool sw = t[b] < t[a];
-        const double ta = sw ? t[b] : t[a], tb = sw ? t[a] : t[b];
+        const bvh_t ta = sw ? t[b] : t[a], tb = sw ? t[a] : t[b];
         const int32_t ca = sw ? c[b] : c[a], cb = sw ? c[a] : c[b];
         t[a] = ta;
         t[b] = tb;
@@ -739,7 +802,7 @@ RT_UNROLL
 // again on pop.  Triangles never return NaN (a NaN ray fails every comparison of triangle_hit and
 // misses).
 RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
-    const d3 inv = d3{1.0 / D.x, 1.0 / D.y, 1.0 / D.z};
+    const BvhRay R = bvh_ray(S, O, D);
     uint64_t stack[BVH_STACK];
     int sp = 0;
     // the node (or leaf) visited next stays in a register: a node's nearest hit child is taken
@@ -759,9 +822,9 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
                 }
             }
         } else {
-            double t[4];
+            bvh_t t[4];
             int32_t c[4];
-            bvh_children(S.bvh[code], O, inv, best, false, t, c);
+            bvh_children(S.bvh[code], R, best, false, t, c);
             if (t[0] != INFINITY) {
                 RT_UNROLL
                 for (int k = 3; k >= 1; --k)
@@ -785,7 +848,7 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
 
 // Any shadowed BVH triangle closer than `stop` along L: returns its distance, else FARAWAY.
 RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
-    const d3 inv = d3{1.0 / L.x, 1.0 / L.y, 1.0 / L.z};
+    const BvhRay R = bvh_ray(S, O, L);
     int32_t stack[BVH_STACK];
     int sp = 0;
     int32_t code = 0;
@@ -800,9 +863,9 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
                 if (t < stop) return t;
             }
         } else {
-            double t[4];
+            bvh_t t[4];
             int32_t c[4];
-            bvh_children(S.bvh[code], O, inv, stop, true, t, c);
+            bvh_children(S.bvh[code], R, stop, true, t, c);
             if (t[0] != INFINITY) {
                 RT_UNROLL
                 for (int k = 3; k >= 1; --k)

@@ -52,6 +52,7 @@ SceneView view_of(const srt_scene_desc* d) {
     S.bvh = g_bvh.nodes.empty() ? nullptr : g_bvh.nodes.data();
     S.bvh_tri = g_bvh.tri.empty() ? nullptr : g_bvh.tri.data();
     S.bvh_nodes = (int)g_bvh.nodes.size();
+    S.bvh_bound = g_bvh.bound;
     S.col = d->colliders; S.mat = d->materials; S.tex = d->textures; S.texels = d->texels;
     S.lights = d->lights; S.media = d->media; S.glossy_f0 = d->glossy_f0; S.light_local = d->light_local;
     S.importance = d->importance;

@@ -64,7 +64,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 848;
+constexpr size_t TRACE_PARAMS_BYTES = 856;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
@@ -1912,7 +1912,7 @@ void mt_gen_launch(srt_ctx* c, const MtArgs& G, int nseg, hipStream_t st, uint32
 
 // Band mode table of one pass shape: the rows' runs of `ns` samples' stored planes, each segment
 // with its jump polynomial x^(2 d0 - 1) mod phi (xpow_mod, ~2.5 ms each, over a few host threads).
-// Regular runs (a shard's 8-row bands: equal length, equal spacing) with short gaps are merged while
+// Regular runs (a shard's row bands: equal length, equal spacing) with short gaps are merged while
 // a segment spans at most MT_MERGE_DOUBLES: it then generates through the other ranks' rows between
 // them (stores masked by band_len / band_period), trading one jump (~110 us of a CU) for a few
 // hundred generated blocks (a CU fraction); other runs are split at `split` doubles (2^18 for a
@@ -2721,6 +2721,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
         S.bvh_tri = (decltype(S.bvh_tri))tri;
         S.bvh = (decltype(S.bvh))nodes;
         S.bvh_nodes = (int)B.nodes.size();
+        S.bvh_bound = B.bound;
         for (int k : B.lin) lin_tri |= d->colliders[k].type == SRT_TRIANGLE;
     }
     int fan = 1;

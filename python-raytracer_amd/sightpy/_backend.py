@@ -346,7 +346,8 @@ def render_scene(scene, spp, jitter=None, seed=None, batch_size=None, rows=None,
 
 
 def render_group(scene, spp, seed=None, batch_size=None, want_rgb=True, mt=True):
-    """Scene.render on every GPU of devices(): each renders its 8-row bands (SRT_RENDER_SHARDED) and
+    """Scene.render on every GPU of devices(): each renders its row bands (SRT_RENDER_SHARDED; at
+    most shard_kmax bands per GPU, rt_device.h shard_band_height: 27 rows at 1080p on 8 GPUs) and
     the tiles are gathered to the first over RCCL (srt_render_group).  `mt`: numpy's stream as in
     render_scene (else the device RNG)."""
     lib, ctxs = group()
