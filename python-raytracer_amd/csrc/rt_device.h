@@ -672,37 +672,42 @@ RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear)
 // The same slab test in f32 arithmetic (half the registers and VALU cycles of the f64 test above,
 // which the RT_BVH_F64 experiment build keeps), widened so that it never rejects a box the exact
 // test accepts.  Per ray and axis: iv = f32(1/D), noiv = -f32(O/D), so a slab plane's distance is
-// one fma, fma(x, iv, noiv) -- within 2.001 * 2^-24 * |1/D| * (|x| + |O|) of (x - O)/D, x a box bound
-// (|x| <= S.bvh_bound).  Each axis's entry / exit is then moved out by e = 2^-20 |1/D| (bound + |O|),
-// 8x that error bound (and the f32 rounding of the subtraction / addition), so the f32 interval holds
-// the exact one, and `tnear` is a lower bound of the exact entry distance.  An axis whose
-// |1/D| (bound + |O|) is not below 1e37 (an axis-parallel ray: 1/D = inf; NaN) constrains nothing
-// (conservative), which also keeps every product finite.
+// one fma, fma(x, iv, noiv) -- within 2.001 * 2^-24 * s of (x - O)/D, s = |1/D| (bound + |O|) and x
+// a box bound (|x| <= S.bvh_bound).  The box's entry / exit (max / min over the axes) are then moved
+// out by e = 2^-20 max(s) over the axes, 8x every axis's error bound and 16x the f32 rounding of the
+// subtraction / addition (|entry| <= 2^20 e), so the f32 interval holds the exact one and `tnear`
+// is a lower bound of the exact entry distance.  An axis whose s is not below 1e37 (an
+// axis-parallel ray: 1/D = inf; NaN) constrains nothing (conservative): its noiv is a quiet NaN,
+// which fminf / fmaxf (IEEE minNum / maxNum) pass over; every other product stays finite.
 #ifndef RT_BOX_MARGIN
 #define RT_BOX_MARGIN 0x1p-20  // (tests/test_mesh.py checks that 0 fails the conservativeness probe)
 #endif
 struct BoxRay {
-    float iv[3], noiv[3], e[3];
+    float iv[3], noiv[3], e;
 };
 RT_HD BoxRay box_ray(d3 O, d3 inv, float bound) {
     BoxRay r;
     const double o[3] = {O.x, O.y, O.z}, iv[3] = {inv.x, inv.y, inv.z};
+    double smax = 0.0;
     for (int a = 0; a < 3; ++a) {
         const double s = fabs(iv[a]) * ((double)bound + fabs(o[a]));
         const bool ok = s < 1e37;
         r.iv[a] = ok ? (float)iv[a] : 0.0f;
-        r.noiv[a] = ok ? -(float)(o[a] * iv[a]) : 0.0f;
-        r.e[a] = ok ? (float)(RT_BOX_MARGIN * s) : INFINITY;
+        r.noiv[a] = ok ? -(float)(o[a] * iv[a]) : __builtin_nanf("");
+        smax = ok ? fmax(smax, s) : smax;
     }
+    r.e = (float)(RT_BOX_MARGIN * smax);
     return r;
 }
 RT_HD bool box4f_hit(const RT_RO BvhNode& nd, int k, const BoxRay& r, float& tnear) {
     float t0 = -INFINITY, t1 = INFINITY;
     for (int a = 0; a < 3; ++a) {
         const float p = fmaf(nd.lo[a][k], r.iv[a], r.noiv[a]), q = fmaf(nd.hi[a][k], r.iv[a], r.noiv[a]);
-        t0 = fmaxf(t0, fminf(p, q) - r.e[a]);
-        t1 = fminf(t1, fmaxf(p, q) + r.e[a]);
+        t0 = fmaxf(t0, fminf(p, q));
+        t1 = fminf(t1, fmaxf(p, q));
     }
+    t0 -= r.e;
+    t1 += r.e;
     tnear = t0;
     return t0 <= t1 && t1 >= 0.0f;
 }
