@@ -7,7 +7,7 @@
 // (smallest distance, then lowest collider index, ties recorded), so results equal the linear loop
 // over `scene.collider_list` (ray.py:124-132).
 //
-// Build: a binary BVH by binned SAH (16 bins on the longest centroid axis), leaves of at most 4
+// Build: a binary BVH by binned SAH (16 bins on the longest centroid axis), leaves of at most 2
 // triangles, depth capped at BVH_MAX_DEPTH; then collapsed into 4-wide nodes (rt_device.h BvhNode):
 // a node's slots are its grandchildren (a leaf child stands for itself), so every 4-wide level spans
 // two binary levels and the traversal stack stays within BVH_STACK.  Leaves keep < 64 triangles and
@@ -27,7 +27,10 @@
 namespace rt {
 
 constexpr int BVH_MIN_TRIANGLES = 8;  // fewer triangles stay in the linear collider loop
-constexpr int BVH_LEAF = 4;
+#ifndef RT_BVH_LEAF
+#define RT_BVH_LEAF 2
+#endif
+constexpr int BVH_LEAF = RT_BVH_LEAF;  // triangles per leaf before the split stops (2: profiles/r05_bvh_f32_box_ab.txt; -DRT_BVH_LEAF for experiments)
 constexpr int BVH_MAX_DEPTH = 20;  // binary levels (so at most 10 4-wide levels: 31 stack entries <= BVH_STACK)
 static_assert(3 * ((BVH_MAX_DEPTH + 1) / 2) + 1 <= BVH_STACK, "traversal stack holds the deepest path");
 constexpr int BVH_LEAF_MAX = 63;            // triangles per leaf (6-bit count in the child code)
