@@ -599,6 +599,25 @@ def test_gpu_mesh_nearest_matches_oracle(tmp_path):
     assert np.array_equal(t[hit], near[hit])
 
 
+def test_gpu_bvh_f32_box_test_is_conservative(tmp_path):
+    """The device's f32 BVH box test (NaN-disabled axes, the widened entry / exit) on rays at its
+    error bound (test_mesh._box_edge_rays): the same nearest hits as the oracle's linear loop."""
+    import test_mesh
+
+    path = str(tmp_path / "ico.obj")
+    scenes.write_icosphere_obj(path, subdiv=3)
+    sc = scenes.mesh_scene(path)
+    Oa, Da = test_mesh._box_edge_rays(sc, np.random.default_rng(29))
+    from sightpy import vec3
+
+    t, ids, orient = _backend().nearest_hits(sc, vec3(*Oa), vec3(*Da))
+    near, ref = O.hit_ids(sc, Oa, Da)
+    assert np.array_equal(ids, ref)
+    hit = ref >= 0
+    assert np.array_equal(t[hit], near[hit])
+    assert hit.mean() > 0.3
+
+
 def test_gpu_create_animation_frames(tmp_path, monkeypatch):
     """create_animation (persistent device scene, background frame writer) writes the same frames
     as rendering them one by one."""

@@ -97,17 +97,12 @@ def test_bvh_nearest_equals_linear_and_oracle(obj, obj_ties, which):
         assert not dup & set(ib.tolist())
 
 
-def test_bvh_f32_box_test_is_conservative(obj):
-    """The BVH's box test runs in f32 (rt_device.h box_ray / box4f_hit), widened to hold the exact
-    slab interval: rays whose slab distances sit at the f32 error bound -- starting on the mesh
-    surface (every vertex, centroid and edge point lies on or inside box planes), nearly
-    axis-parallel (1/D up to 1e300, the f32 axis switched off), from far away (|O| = 1e5 with a
-    2-unit mesh) -- give exactly the linear loop's nearest hit."""
-    sc = scenes.mesh_scene(obj[0])
-    rng = np.random.default_rng(23)
+def _box_edge_rays(sc, rng, k=1500):
+    """Rays whose slab distances sit at the f32 box test's error bound: starting on the mesh surface
+    (every vertex, edge and face point lies on or inside box planes), nearly axis-parallel (1/D up
+    to 1e300: the f32 axis switched off), from far away (|O| = 1e5 with a 2-unit mesh)."""
     mesh = [c for c in sc.collider_list if type(c).__name__ == "Triangle_Collider"]
     tri = np.array([[[c.p1.x, c.p1.y, c.p1.z], [c.p2.x, c.p2.y, c.p2.z], [c.p3.x, c.p3.y, c.p3.z]] for c in mesh])
-    k = 1500
     pick = tri[rng.integers(0, len(tri), k)]
     w = rng.dirichlet([1.0, 1.0, 1.0], size=k)
     w[: k // 3] = np.eye(3)[rng.integers(0, 3, k // 3)]  # exactly at vertices
@@ -124,7 +119,14 @@ def test_bvh_f32_box_test_is_conservative(obj):
     Os.append(far), Ds.append(pick.mean(axis=1) - far)
     Oa, Da = np.concatenate(Os), np.concatenate(Ds)
     Da = Da / np.linalg.norm(Da, axis=1, keepdims=True)
-    Oa, Da = np.ascontiguousarray(Oa.T), np.ascontiguousarray(Da.T)
+    return np.ascontiguousarray(Oa.T), np.ascontiguousarray(Da.T)
+
+
+def test_bvh_f32_box_test_is_conservative(obj):
+    """The BVH's box test runs in f32 (rt_device.h box_ray / box4f_hit), widened to hold the exact
+    slab interval: on rays at its error bound it gives exactly the linear loop's nearest hit."""
+    sc = scenes.mesh_scene(obj[0])
+    Oa, Da = _box_edge_rays(sc, np.random.default_rng(23))
     HC.set_bvh(1)
     tb, ib, ob = HC.nearest(sc, Oa, Da)
     HC.set_bvh(0)
