@@ -278,8 +278,8 @@ static_assert(sizeof(SceneView) == 184 && offsetof(SceneView, nlut_lds) == 136, 
 
 // BVH node, 4-wide (128 B: one traversal step loads one cache line and tests four boxes): child k's
 // box [lo[.][k], hi[.][k]] in float, rounded outward from the build's f64 boxes (which are inflated so
-// that rounding never excludes a triangle's hit point), so the f64 slab test on the float bounds is
-// conservative; child[k] >= 0: inner node; child[k] < 0 (and != BVH_EMPTY): leaf of the triangles
+// that rounding never excludes a triangle's hit point), tested by the widened f32 slab test
+// (box4f_hit), which is conservative against the exact test on these bounds; child[k] >= 0: inner node; child[k] < 0 (and != BVH_EMPTY): leaf of the triangles
 // bvh_tri[-child[k] - 1, .. + count[k]); BVH_EMPTY: no child in slot k
 struct BvhNode {
     float lo[3][4], hi[3][4];
