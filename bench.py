@@ -224,6 +224,40 @@ def pmc_counters(config, kernel, variant=None):
     return None, None
 
 
+ROCPROF_TAG = {"example1_1080p_d5": "ex1_1080p_d5", "example3_1080p_d8": "ex3_1080p_d8"}
+
+
+def rocprof_kernel_ms(config, kernel, sync_kind):
+    """The committed rocprofv3 --kernel-trace --stats average of `kernel` (ms) over synchronous frames
+    of this config (profiles/rNN*_<tag>_kernel_stats_<sync_kind>.csv, newest round first), or
+    (None, None): the time base the roofline's HIP-event kernel_ms is checked against."""
+    tag = ROCPROF_TAG.get(config)
+    if tag is None:
+        return None, None
+    for f in sorted(ROOT.glob("profiles/r*_%s_kernel_stats_%s.csv" % (tag, sync_kind)), reverse=True):
+        import csv
+
+        for row in csv.DictReader(open(f)):
+            if (kernel + "<") in row["Name"] and ", true>" not in row["Name"]:
+                return float(row["AverageNs"]) / 1e6, "%s (%s launches)" % (f.name, row["Calls"])
+    return None, None
+
+
+def lane_summary(raw):
+    """srt_debug_lane_stats counters -> per-depth active lane fractions of the depth loop."""
+    out = []
+    for d, (it, lanes) in enumerate(raw):
+        if it:
+            out.append({"depth": d, "wave_iterations": int(it), "live_lanes": int(lanes),
+                        "frac": round(lanes / (64.0 * it), 4)})
+    it_all = sum(x["wave_iterations"] for x in out)
+    return {"per_depth": out,
+            "overall": round(sum(x["live_lanes"] for x in out) / (64.0 * it_all), 4) if it_all else None,
+            "what": "live lanes / (64 x wave iterations) of the fused depth loop, per depth (srt_debug_lane_stats "
+                    "over one pipelined frame); a wave runs a depth while any of its lanes' samples still has a "
+                    "ray there"}
+
+
 def roofline(kname, kms, model_bytes, path, krec, src):
     """The dominant kernel against the MI355X roofline.  achieved = algorithmic bytes / launch time
     (HIP events); traffic = PMC HBM bytes per launch; the arithmetic intensity (counted fp64 FLOP per
@@ -251,6 +285,12 @@ def roofline(kname, kms, model_bytes, path, krec, src):
         roof["ridge_flop_per_byte"] = round(ridge, 2)
         roof["fp64"] = {"achieved_TFLOPs": round(tf, 3), "peak": FP64_PEAK_TFS, "frac": round(tf / FP64_PEAK_TFS, 4),
                         "note": "64 x (ADD + MUL + TRANS + 2 FMA) f64 wave instructions: counts masked lanes"}
+        if krec.get("valu_lane_util") is not None:
+            # the flops the active lanes executed: the count weighted by the VALU instructions' active
+            # lanes (SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU)
+            u = krec["valu_lane_util"]
+            roof["fp64"].update({"valu_lane_util": round(u, 4), "achieved_TFLOPs_active_lanes": round(tf * u, 3),
+                                 "frac_active_lanes": round(tf * u / FP64_PEAK_TFS, 4)})
         if ai >= ridge:
             # the fp64 side of the ridge: the kernel is measured against the vector fp64 peak (there is
             # no MFMA work here); the HBM figures stay beside it
@@ -748,6 +788,14 @@ def main():
             N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n1)))
             if n1.value > n0.value:
                 sec["stats_lean"] = lean_stats
+                # lane utilisation of the pipelined frames' depth loop: one more pipelined frame with the
+                # kernel's counting instantiation (not timed)
+                raw = (ctypes.c_int64 * (2 * 16))()
+                N.check(lib, lib.srt_debug_lane_stats(ctx, 1, None, 0))
+                step()
+                step()
+                N.check(lib, lib.srt_debug_lane_stats(ctx, 0, raw, 16))
+                sec["lane_stats"] = lane_summary([(raw[2 * d] / 2, raw[2 * d + 1] / 2) for d in range(16)])
         if world == 1 and rows32 is None:
             # the round-1 headline form: jitter resident in HBM, outputs left in HBM
             nj = spp * 4 * npix_full
@@ -860,6 +908,19 @@ def main():
                                            "synchronous frames (option sync_lean)")
                 roof["sync_frames_kernel"] = {"kernel": "k_primary (fused paths: synchronous frames, Scene.render)",
                                               "kernel_ms": round(kms_sync / 1.0, 4)}
+            rp_ms, rp_src = (None, None) if (args.size or args.spp or world > 1 or rows32 is not None) else \
+                rocprof_kernel_ms(args.config, kname, "sync_lean" if kname == "k_primary_lean" else "sync")
+            if rp_ms is not None:
+                # the same launch's rocprofv3 dispatch time (the events bracket it ~0.05 ms wider)
+                roof["kernel_ms_rocprof"] = round(rp_ms, 4)
+                roof["kernel_ms_rocprof_source"] = rp_src
+                if "fp64" in roof:
+                    f = roof["fp64"]
+                    f["frac_rocprof"] = round(f["frac"] * kms / rp_ms, 4)
+                    if "frac_active_lanes" in f:
+                        f["frac_active_lanes_rocprof"] = round(f["frac_active_lanes"] * kms / rp_ms, 4)
+            if "lane_stats" in sec:
+                roof["active_lane_frac"] = sec["lane_stats"]
             rec["roofline"] = roof
         if not args.no_cpu_baseline and world == 1 and args.config in CPU_SKIP:
             rec["cpu_baseline"] = {"value": None, "skipped": CPU_SKIP[args.config]}

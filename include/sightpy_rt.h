@@ -410,6 +410,13 @@ int srt_debug_mt_residue(srt_ctx* ctx, int64_t* nonzero_words);
 /* Diagnostic: renders that found their generation queued by srt_render_prefetch (used, not
  * launched again) and prefetches queued, since the context was created. */
 int srt_debug_prefetch_counts(srt_ctx* ctx, int64_t* used, int64_t* queued);
+/* Diagnostic: lane utilisation of the lean fused kernel's depth loop (k_primary_lean: the headline's
+ * pipelined frames, or synchronous ones with option "sync_lean"; ray.py:122-148's recursion traced in
+ * one thread per sample; while counting, the kernel's counting instantiation runs).  mode 1 zeroes
+ * and starts the counters for the frames rendered next; mode 0 waits for them and writes out[d][0]
+ * = wave iterations that traced depth d, out[d][1] = live lanes in those iterations (d < n <=
+ * SRT_MAX_DEPTHS), then stops counting.  active lane fraction(d) = out[d][1] / (64 out[d][0]). */
+int srt_debug_lane_stats(srt_ctx* ctx, int mode, int64_t* out, int n);
 /* Diagnostic: launches of the lean fused kernel (k_primary_lean: pipelined frames of single-child
  * scenes without a BVH, or any frame with option "sync_lean") since the context was created. */
 int srt_debug_lean_launches(srt_ctx* ctx, int64_t* launches);

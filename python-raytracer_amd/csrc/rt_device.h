@@ -677,8 +677,10 @@ RT_HD bool box4_hit(const RT_RO BvhNode& nd, int k, d3 O, d3 inv, double& tnear)
 // out by e = 2^-20 max(s) over the axes, 8x every axis's error bound and 16x the f32 rounding of the
 // subtraction / addition (|entry| <= 2^20 e), so the f32 interval holds the exact one and `tnear`
 // is a lower bound of the exact entry distance.  An axis whose s is not below 1e37 (an
-// axis-parallel ray: 1/D = inf; NaN) constrains nothing (conservative): its noiv is a quiet NaN,
-// which fminf / fmaxf (IEEE minNum / maxNum) pass over; every other product stays finite.
+// axis-parallel ray: 1/D = inf; NaN) or whose 1/D does not fit a float (|D| < ~3e-39 on a tiny mesh
+// near the origin, where s stays small but f32(1/D) would be inf) constrains nothing
+// (conservative): its noiv is a quiet NaN, which fminf / fmaxf (IEEE minNum / maxNum) pass over;
+// every other product stays finite.
 #ifndef RT_BOX_MARGIN
 #define RT_BOX_MARGIN 0x1p-20  // (tests/test_mesh.py checks that 0 fails the conservativeness probe)
 #endif
@@ -691,7 +693,7 @@ RT_HD BoxRay box_ray(d3 O, d3 inv, float bound) {
     double smax = 0.0;
     for (int a = 0; a < 3; ++a) {
         const double s = fabs(iv[a]) * ((double)bound + fabs(o[a]));
-        const bool ok = s < 1e37;
+        const bool ok = s < 1e37 && fabs(iv[a]) < 3e38;
         r.iv[a] = ok ? (float)iv[a] : 0.0f;
         r.noiv[a] = ok ? -(float)(o[a] * iv[a]) : __builtin_nanf("");
         smax = ok ? fmax(smax, s) : smax;

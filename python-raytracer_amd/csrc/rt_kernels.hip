@@ -64,7 +64,7 @@ constexpr int BLOCK = 256;
 // device-scope atomics executed at the memory side; with 16 counters their serialisation cost the
 // depth-0 kernel ~40 % (1.39 vs 0.87 ms, ex1 1080p), 64-256 counters remove it.
 constexpr int NSHARD = RT_NSHARD;
-constexpr size_t TRACE_PARAMS_BYTES = 856;
+constexpr size_t TRACE_PARAMS_BYTES = 864;
 constexpr int MAX_LUT_LDS = 12;  // texture tables staged in LDS per block (2 KiB each)
 // retry bits of flags[1]: a queue shard / ring overflowed (re-render with bigger queues); a tie gave
 // a chained ray a second child (re-render without chain mode)
@@ -124,6 +124,9 @@ struct TraceParams {
     double* fbg;
     int groups;
     int ntiles;
+    // srt_debug_lane_stats: [depth][2] u64 = (wave iterations that traced the depth, live lanes in
+    // them) of the fused paths' depth loop, or null (counting off)
+    unsigned long long* lane_stats;
 };
 // kernel argument: host and device passes must agree on the layout (catches address-space pointer
 // size differences, see SceneView)
@@ -603,6 +606,15 @@ struct FusedEmit {
     }
 };
 
+// srt_debug_lane_stats: one wave iteration of a depth with the live lanes m, counted by the lowest
+// live lane ([0] iterations, [1] live lanes)
+__device__ __forceinline__ void lane_count(unsigned long long* st, uint64_t m) {
+    if (lanes_below(m) == 0) {
+        atomicAdd(st, 1ull);
+        atomicAdd(st + 1, (unsigned long long)__builtin_popcountll(m));
+    }
+}
+
 // Copy the first `nlut` texture lookup tables into LDS (dynamic shared memory) and point the
 // scene view at them: texel -> value becomes an LDS read instead of a dependent global load.
 __device__ __forceinline__ void stage_luts(const TraceParams& P) {
@@ -640,7 +652,7 @@ __device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3]
 // to the depth-1 queue for k_trace.
 template <uint32_t MATS, int OCC = 2, bool FUSE = false>
 __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
-    constexpr bool LEAN = false;
+    constexpr bool LEAN = false, LANE_STATS = false;
 #include "rt_primary_body.inc"
 }
 
@@ -653,7 +665,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_primary(TraceParams P0) {
 // and jitter per sample (LEAN), which holds its spills to the 168-VGPR build's.  Same box, ex1 1080p d5
 // 6 spp pipelined frames 0.901 -> 0.876 ms; the kernel alone (device-resident frames) 0.752 -> 0.762
 // (profiles/r05_lean_primary_ab.txt).
-template <uint32_t MATS, int OCC>
+// LANE_STATS: the instantiation srt_debug_lane_stats selects (the counting cost 2 spilled VGPRs as a
+// run-time branch in the default kernels).
+template <uint32_t MATS, int OCC, bool LANE_STATS = false>
 __global__ __launch_bounds__(BLOCK, OCC) __attribute__((amdgpu_num_vgpr(80))) void k_primary_lean(TraceParams P0) {
     constexpr bool FUSE = true, LEAN = true;
 #include "rt_primary_body.inc"
@@ -989,6 +1003,7 @@ struct Variant {
     // k_primary_lean (160 VGPRs): the fused paths of pipelined frames, whose numpy-stream generators
     // then run beside them (mt_gen_launch); synchronous frames take `fused`
     void (*lean)(TraceParams) = nullptr;
+    void (*lean_stats)(TraceParams) = nullptr;  // k_primary_lean<.., LANE_STATS> (srt_debug_lane_stats)
 };
 // occupancy experiments for the headline scene (srt_set_option "occupancy" = k in 2..4 selects the
 // build for k waves/SIMD, OCC_VARIANTS[k - 2]; built with -DRT_OCC_VARIANTS); the default
@@ -1015,7 +1030,8 @@ constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (regi
 #endif
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
-     k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>, k_primary_lean<MATS_GLOSSY_SKY, RT_FUSE_OCC>},
+     k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>, k_primary_lean<MATS_GLOSSY_SKY, RT_FUSE_OCC>,
+     k_primary_lean<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>},
 #ifndef RT_EXP_MIN  // (register-usage experiments, tools/resource_usage.py: the headline variants only, a quicker compile)
     {MATS_DIELECTRIC, k_primary<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC>, k_frame<MATS_DIELECTRIC, OCC>, k_trace<MATS_DIELECTRIC, OCC, true>},
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
@@ -1049,7 +1065,8 @@ constexpr uint32_t seq_bits(std::initializer_list<int> t) {
 constexpr uint32_t MATS_SEQ_SSPC = MATS_GLOSSY_SKY | seq_bits({SRT_SPHERE, SRT_SPHERE, SRT_PLANE, SRT_CUBOID});
 const Variant SEQ_VARIANTS[] = {
     {MATS_SEQ_SSPC, k_primary<MATS_SEQ_SSPC, OCC>, k_trace<MATS_SEQ_SSPC, OCC>, k_frame<MATS_SEQ_SSPC, OCC>,
-     k_trace<MATS_SEQ_SSPC, OCC, true>, k_primary<MATS_SEQ_SSPC, RT_FUSE_OCC, true>, k_primary_lean<MATS_SEQ_SSPC, RT_FUSE_OCC>},
+     k_trace<MATS_SEQ_SSPC, OCC, true>, k_primary<MATS_SEQ_SSPC, RT_FUSE_OCC, true>, k_primary_lean<MATS_SEQ_SSPC, RT_FUSE_OCC>,
+     k_primary_lean<MATS_SEQ_SSPC, RT_FUSE_OCC, true>},
 };
 #endif
 const Variant& pick_variant(uint32_t mats, uint32_t seq = 0) {
@@ -1613,6 +1630,7 @@ struct srt_ctx {
         hipStream_t gen_on = nullptr;
     } pf;
     int64_t pf_used = 0, pf_queued = 0;  // (srt_debug_prefetch_counts)
+    unsigned long long* lane_stats = nullptr;  // (srt_debug_lane_stats) [SRT_MAX_DEPTHS][2] or null
 };
 
 namespace {
@@ -1768,6 +1786,7 @@ TraceParams base_params(srt_ctx* c, uint64_t seed) {
     P.shadow = c->f->shadow;
     P.seg = c->f->seg;
     P.seed = seed;
+    P.lane_stats = c->lane_stats;  // (read by k_primary_lean<.., true> only)
     return P;
 }
 
@@ -2423,7 +2442,7 @@ int srt_destroy(srt_ctx* c) {
     for (hipStream_t g : c->gen_streams)
         if (g) (void)hipStreamDestroy(g);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_y};
+    void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_y, c->lane_stats};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (auto& t : c->mt_bandtabs) {
@@ -3291,7 +3310,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
                                         : n_rows == Hf && c->lean_blocks > 0              ? c->lean_blocks
                                         : n_rows < Hf && c->lean_blocks_shard > 0         ? c->lean_blocks_shard
                                                                                             : c->max_blocks);
-            hipLaunchKernelGGL(F.fuse ? (lean ? V.lean : V.fused) : V.primary,
+            hipLaunchKernelGGL(F.fuse ? (lean ? (c->lane_stats && V.lean_stats ? V.lean_stats : V.lean) : V.fused) : V.primary,
                                dim3(grid_for(((npix * P.pix_groups + 63) / 64) * 64, pgrid)), dim3(BLOCK),
                                lut_bytes(c), c->f->stream, P);
             HIP_TRY(hipGetLastError());
@@ -4176,6 +4195,27 @@ int srt_debug_prof(srt_ctx* c, unsigned long long* out, int reset) {
 int srt_debug_lean_launches(srt_ctx* c, int64_t* launches) {
     if (!c || !launches) return fail(SRT_ERR_ARG, "null argument");
     *launches = c->lean_launches;
+    return SRT_OK;
+}
+
+int srt_debug_lane_stats(srt_ctx* c, int mode, int64_t* out, int n) {
+    if (!c) return fail(SRT_ERR_ARG, "null ctx");
+    if (mode != 0 && mode != 1) return fail(SRT_ERR_ARG, "lane stats mode: 1 start, 0 read and stop");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = finish_async(c, nullptr);  // (the frames in flight were queued with the old pointer)
+    if (rc) return rc;
+    const size_t bytes = (size_t)SRT_MAX_DEPTHS * 2 * sizeof(unsigned long long);
+    if (mode == 1) {
+        if (!c->lane_stats) HIP_TRY(hipMalloc(&c->lane_stats, bytes));
+        HIP_TRY(hipMemset(c->lane_stats, 0, bytes));
+        return SRT_OK;
+    }
+    if (!out || n < 0 || n > SRT_MAX_DEPTHS) return fail(SRT_ERR_ARG, "lane stats: out[n][2], n <= SRT_MAX_DEPTHS");
+    if (!c->lane_stats) return fail(SRT_ERR_ARG, "lane stats were not started");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, c->lane_stats, (size_t)n * 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(c->lane_stats));
+    c->lane_stats = nullptr;
     return SRT_OK;
 }
 

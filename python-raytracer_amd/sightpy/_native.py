@@ -236,6 +236,7 @@ SIGNATURES = {
     "srt_synchronize": (ctypes.c_int, [_p]),
     "srt_debug_mt_residue": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int64)]),
     "srt_debug_prefetch_counts": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "srt_debug_lane_stats": (ctypes.c_int, [_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "srt_debug_lean_launches": (ctypes.c_int, [_p, ctypes.POINTER(ctypes.c_int64)]),
     "srt_render_prefetch": (ctypes.c_int, [_p, ctypes.POINTER(CameraDesc), ctypes.POINTER(RenderArgs)]),
     "srt_render_finish": (ctypes.c_int, [_p, ctypes.POINTER(Stats)]),

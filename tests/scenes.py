@@ -200,7 +200,7 @@ def write_icosphere_obj(path, subdiv=2, radius=0.5, duplicate_faces=0, slash_for
     return len(F)
 
 
-def mesh_scene(obj_path, width=64, height=48, depth=3):
+def mesh_scene(obj_path, width=64, height=48, depth=3, center=(0.35, 0.05, -1.0)):
     """A TriangleMesh in the ex1 setting: a glossy icosphere mesh next to a
     sphere over the textured floor, sky box background, one shadowing light."""
     red = Glossy(diff_color=rgb(0.6, 0.1, 0.1), n=vec3(1.5 + 0.2j, 1.5 + 0.2j, 1.5 + 0.2j), roughness=0.2,
@@ -214,7 +214,7 @@ def mesh_scene(obj_path, width=64, height=48, depth=3):
                   screen_height=height)
     sc.add_DirectionalLight(Ldir=vec3(0.52, 0.45, -0.5), color=rgb(0.5, 0.5, 0.5))
     sc.add(Sphere(material=gold, center=vec3(-0.8, 0.0, -1.2), radius=0.45, max_ray_depth=depth))
-    sc.add(TriangleMesh(obj_path, center=vec3(0.35, 0.05, -1.0), material=red, max_ray_depth=depth))
+    sc.add(TriangleMesh(obj_path, center=vec3(*center), material=red, max_ray_depth=depth))
     sc.add(Plane(material=floor, center=vec3(0, -0.5, -2.0), width=40.0, height=40.0, u_axis=vec3(1.0, 0, 0),
                  v_axis=vec3(0, 0, -1.0), max_ray_depth=depth))
     sc.add_Background("stormydays.png")

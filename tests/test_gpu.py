@@ -277,6 +277,38 @@ def test_example1_1080p_d5_ray_counts_match_reference_survey():
     assert out.stats["rays_per_depth"] == [12441600, 6413569, 1326285, 537874, 163811, 95648]
 
 
+def test_gpu_lane_stats_count_the_depth_loop():
+    """srt_debug_lane_stats on the headline frame's lean kernel (its counting instantiation): the live
+    lanes of each depth are exactly the rays entering that depth (the reference's per-depth counts),
+    depth 0 runs one wave iteration per 32 pixels x 3 samples (two sample groups), and the image is
+    the non-counting kernel's bit for bit."""
+    import ctypes
+    from sightpy import _native as N
+
+    sc = scenes.example1(1920, 1080, 5)
+    np.random.seed(0)
+    jit = sc.camera.draw_jitter(6)
+    lib, ctx = _backend().context()
+    N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 1))
+    raw = (ctypes.c_int64 * 32)()
+    try:
+        plain = _backend().render_scene(sc, 6, jitter=jit, seed=1)
+        N.check(lib, lib.srt_debug_lane_stats(ctx, 1, None, 0))
+        out = _backend().render_scene(sc, 6, jitter=jit, seed=1)
+        N.check(lib, lib.srt_debug_lane_stats(ctx, 0, raw, 16))
+    finally:
+        N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 0))
+    assert out.stats["kernel_path"] == "fused"
+    assert np.array_equal(out.rgb, plain.rgb) and np.array_equal(out.srgb8, plain.srgb8)
+    rpd = out.stats["rays_per_depth"]
+    assert [raw[2 * d + 1] for d in range(len(rpd))] == rpd
+    assert raw[0] == 1920 * 1080 // 32 * 3
+    for d in range(len(rpd)):
+        assert 64 * raw[2 * d] >= raw[2 * d + 1] > 0
+    assert raw[2 * len(rpd)] == 0
+    assert lib.srt_debug_lane_stats(ctx, 0, raw, 16) != 0  # (stopped: nothing to read)
+
+
 def test_example3_1080p_d8_counts_match_reference_survey():
     sc = scenes.example3(1920, 1080, 8)
     np.random.seed(0)
@@ -616,6 +648,25 @@ def test_gpu_bvh_f32_box_test_is_conservative(tmp_path):
     hit = ref >= 0
     assert np.array_equal(t[hit], near[hit])
     assert hit.mean() > 0.3
+
+
+def test_gpu_bvh_f32_box_test_tiny_mesh(tmp_path):
+    """A mesh ~1e-2 across at the origin and direction components ~1e-39 (f32(1/D) overflows while
+    the 1e37 guard passes: test_mesh._tiny_mesh_rays): the device's nearest hits equal the oracle's."""
+    import test_mesh
+
+    path = str(tmp_path / "ico_tiny.obj")
+    scenes.write_icosphere_obj(path, subdiv=3, radius=5e-3)
+    sc = scenes.mesh_scene(path, center=(0.0, 0.0, 0.0))
+    Oa, Da = test_mesh._tiny_mesh_rays(sc, np.random.default_rng(37))
+    from sightpy import vec3
+
+    t, ids, orient = _backend().nearest_hits(sc, vec3(*Oa), vec3(*Da))
+    near, ref = O.hit_ids(sc, Oa, Da)
+    assert np.array_equal(ids, ref)
+    hit = ref >= 0
+    assert np.array_equal(t[hit], near[hit])
+    assert (ref >= 1).mean() > 0.3
 
 
 def test_gpu_create_animation_frames(tmp_path, monkeypatch):

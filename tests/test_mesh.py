@@ -122,6 +122,50 @@ def _box_edge_rays(sc, rng, k=1500):
     return np.ascontiguousarray(Oa.T), np.ascontiguousarray(Da.T)
 
 
+def _tiny_mesh_rays(sc, rng, k=3000):
+    """Rays through a mesh ~1e-2 across at the origin with one direction component ~1e-39: that
+    axis's s = |1/D| (bound + |O|) stays below the 1e37 guard while f32(1/D) overflows to inf
+    (the axis must then constrain nothing, as for axis-parallel rays)."""
+    Os, Ds = [], []
+    for a in range(3):
+        O = rng.uniform(-4e-3, 4e-3, size=(k, 3))
+        b = (a + 1) % 3
+        O[:, b] = rng.choice([-0.02, 0.02], k)  # outside the mesh along axis b, aimed back through it
+        D = rng.normal(scale=0.3, size=(k, 3))
+        D[:, b] = -np.sign(O[:, b])
+        D[:, a] = rng.choice([1e-39, -1e-39, 3e-39], k)
+        Os.append(O), Ds.append(D)
+    Oa, Da = np.concatenate(Os), np.concatenate(Ds)
+    Da = Da / np.linalg.norm(Da, axis=1, keepdims=True)
+    return np.ascontiguousarray(Oa.T), np.ascontiguousarray(Da.T)
+
+
+@pytest.fixture(scope="module")
+def tiny_obj(tmp_path_factory):
+    p = tmp_path_factory.mktemp("mesh") / "icosphere_tiny.obj"
+    scenes.write_icosphere_obj(str(p), subdiv=2, radius=5e-3)
+    return str(p)
+
+
+def test_bvh_f32_box_test_tiny_mesh_overflowing_inverse(tiny_obj):
+    """A direction component whose f32 inverse overflows on a mesh ~1e-2 across at the origin: the
+    BVH gives exactly the linear loop's nearest hits (before the |1/D| < 3e38 guard in box_ray the
+    boxes beside the ray's origin on that axis were dropped)."""
+    sc = scenes.mesh_scene(tiny_obj, center=(0.0, 0.0, 0.0))
+    Oa, Da = _tiny_mesh_rays(sc, np.random.default_rng(31))
+    HC.set_bvh(1)
+    tb, ib, ob = HC.nearest(sc, Oa, Da)
+    HC.set_bvh(0)
+    try:
+        tl, il, ol = HC.nearest(sc, Oa, Da)
+    finally:
+        HC.set_bvh(1)
+    assert np.array_equal(ib, il)
+    assert np.array_equal(tb, tl, equal_nan=True)
+    assert np.array_equal(ob, ol, equal_nan=True)
+    assert (ib >= 1).mean() > 0.3
+
+
 def test_bvh_f32_box_test_is_conservative(obj):
     """The BVH's box test runs in f32 (rt_device.h box_ray / box4f_hit), widened to hold the exact
     slab interval: on rays at its error bound it gives exactly the linear loop's nearest hit."""

@@ -56,6 +56,8 @@ for step in "$@"; do
     api_prof) run api_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/api_prof -o api --output-format csv -- python3 tools/api_timing.py --repeats 5 ;;
     shardprof) run shardprof_${SHARD:-8}_r${SHARD_RANK:-0} 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/shardprof_${SHARD:-8}_r${SHARD_RANK:-0} -o s --output-format csv -- python3 bench.py --config ${CONFIG:-example1_1080p_d5} --steps 20 --warmup 2 --no-cpu-baseline --no-secondary --shard-of ${SHARD:-8} --shard-rank ${SHARD_RANK:-0} ;;
     profsync) run profsync 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsync -o bench --output-format csv -- python3 bench.py --sync --no-cpu-baseline --no-secondary ;;
+    profsync_lean) run profsync_lean 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profsync_lean -o bench --output-format csv -- python3 bench.py --sync --option sync_lean=1 --no-cpu-baseline --no-secondary --steps ${STEPS:-45} --warmup 5 ;;
+    driver) run driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     rngdev) run bench_rngdev 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --rng device ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -19,6 +19,9 @@ launch (MI355X_MICROARCH.md § HBM and § Execution model):
   valu_active_frac = 4 x SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)
                   cycles waves spent issuing VALU (summed over waves) over the SIMD cycles
   wave_wait_frac  = SQ_WAIT_ANY / SQ_WAVE_CYCLES
+  valu_lane_util  = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)
+                  the active lanes of the VALU instructions (rocprofv3's VALUUtilization): the
+                  fraction of the fp64_flop upper bound that lanes really executed
 
     python tools/pmc_summary.py gpurun_out/pmc_a gpurun_out/pmc_b ... --out profiles/r03_counters_X.json
     python tools/pmc_summary.py --recompute profiles/r02_counters_X.json ...   (derived fields again
@@ -59,7 +62,8 @@ DERIVED = {"traffic_bytes": "2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024",
                               % (XCDS, SIMDS),
            "valu_active_frac": "4 x SQ_ACTIVE_INST_VALU (quad-cycles) / (GRBM_GUI_ACTIVE / %d XCDs x %d SIMDs)"
                                % (XCDS, SIMDS),
-           "wave_wait_frac": "SQ_WAIT_ANY / SQ_WAVE_CYCLES"}
+           "wave_wait_frac": "SQ_WAIT_ANY / SQ_WAVE_CYCLES",
+           "valu_lane_util": "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (rocprofv3 VALUUtilization)"}
 
 
 def derive(c):
@@ -80,6 +84,8 @@ def derive(c):
         rec["valu_active_frac"] = 4 * c["SQ_ACTIVE_INST_VALU"] / cyc
     if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
         rec["wave_wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
+        rec["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"])
     return rec
 
 
@@ -88,7 +94,7 @@ def recompute(paths):
         out = json.load(open(p))
         out["derived"] = DERIVED
         for k, rec in out["kernels"].items():
-            for key in ("valu_issue_frac", "valu_active_frac", "wave_wait_frac"):
+            for key in ("valu_issue_frac", "valu_active_frac", "wave_wait_frac", "valu_lane_util"):
                 rec.pop(key, None)
             rec.update(derive(rec["counters"]))
         with open(p, "w") as fh:
