@@ -411,7 +411,7 @@ def run_group(args, gpus):
     (SRT_RENDER_RGB_ROWS).  Returns the JSON record (without the CPU baseline)."""
     import scenes
     from sightpy import _backend as B, _native as N
-    from sightpy._shard import SHARD_SNAKE, band_height, scene_fanout, shard_kmax
+    from sightpy._shard import band_height, scene_fanout, shard_kmax
 
     builder, W, H, depth, spp, label = CONFIGS[args.config]
     if args.spp:
@@ -432,8 +432,6 @@ def run_group(args, gpus):
         N.check(lib, lib.srt_set_option(c, b"pipeline", 1))
         if args.shard_bands:
             N.check(lib, lib.srt_set_option(c, b"shard_bands", args.shard_bands))
-        if args.shard_snake >= 0:
-            N.check(lib, lib.srt_set_option(c, b"shard_snake", args.shard_snake))
         for kv in args.option:
             k, v = kv.split("=")
             N.check(lib, lib.srt_set_option(c, k.encode(), int(v)))
@@ -507,10 +505,8 @@ def run_group(args, gpus):
                                                   else "every GPU's rows of the linear RGB (f64) stored in its HBM"),
                    "frame_ms": round(ms_step, 4),
                    "row_bands": {"kmax": shard_kmax(H, gpus, args.shard_bands, scene_fanout(sc)),
-                                 "snake": args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE,
                                  "band_height": band_height(H, gpus, shard_kmax(H, gpus, args.shard_bands,
-                                                                                scene_fanout(sc)),
-                                                            args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE)}},
+                                                                                scene_fanout(sc)))}},
     }
     if not args.no_secondary:
         if not args.rgb_to_host:
@@ -573,8 +569,6 @@ def main():
                          "does after the RCCL gather (library option rehearse_assemble)")
     ap.add_argument("--shard-bands", type=int, default=0,
                     help="most row bands per rank (library option shard_bands; default rt_device.h shard_kmax)")
-    ap.add_argument("--shard-snake", type=int, default=-1,
-                    help="band dealing order, 0 round-robin / 1 snake (library option shard_snake; default SHARD_SNAKE)")
     args = ap.parse_args()
     if not 1 <= args.hw_queues <= 32:
         raise SystemExit("bench.py: --hw-queues 1 .. 32")
@@ -622,8 +616,6 @@ def main():
     N.check(lib, lib.srt_set_option(ctx, b"pipeline", 1))  # size every frame slot during the warmup
     if args.shard_bands:
         N.check(lib, lib.srt_set_option(ctx, b"shard_bands", args.shard_bands))
-    if args.shard_snake >= 0:
-        N.check(lib, lib.srt_set_option(ctx, b"shard_snake", args.shard_snake))
     for kv in args.option:
         k, v = kv.split("=")
         N.check(lib, lib.srt_set_option(ctx, k.encode(), int(v)))
@@ -637,16 +629,15 @@ def main():
     def frame_flags(host_rgb):
         return base_flags | ((N.RENDER_RGB_ROWS if world > 1 else 0) if host_rgb else N.RENDER_RGB_LOCAL)
     rows32 = None
-    from sightpy._shard import SHARD_SNAKE, band_height, scene_fanout, shard_kmax, shard_rows
+    from sightpy._shard import band_height, scene_fanout, shard_kmax, shard_rows
 
     # the library's band count (rt_device.h shard_kmax: depends on the scene's fan-out)
     kmax = shard_kmax(H, max(world, args.shard_of, 1), args.shard_bands, scene_fanout(sc))
-    snake = args.shard_snake if args.shard_snake >= 0 else SHARD_SNAKE
     rehearse = {None: None}  # rank -> its rows (None: the frame as the launcher splits it)
     if args.shard_of > 1 and world == 1:
         ranks = (range(args.shard_of) if args.shard_rank == "all" else
                  range(args.shard_of - 1, -1, -1) if args.shard_rank == "all-reversed" else [int(args.shard_rank)])
-        rehearse = {r: np.ascontiguousarray(shard_rows(H, args.shard_of, r, kmax, snake), dtype=np.int32)
+        rehearse = {r: np.ascontiguousarray(shard_rows(H, args.shard_of, r, kmax), dtype=np.int32)
                     for r in ranks}
         rows32 = rehearse[min(ranks)]
         npix_full = max(len(v) for v in rehearse.values()) * W  # the shards' outputs
@@ -863,8 +854,8 @@ def main():
                                    "returns the uint8 image, scene.py:118-140)"),
                        "frame_ms": round(ms_step, 4),
                        "host_enqueue_ms": round(max(enq), 4),
-                       "row_bands": {"kmax": kmax, "snake": snake,
-                                     "band_height": band_height(H, max(world, args.shard_of, 1), kmax, snake)}},
+                       "row_bands": {"kmax": kmax,
+                                     "band_height": band_height(H, max(world, args.shard_of, 1), kmax)}},
         }
         if len(rehearse) > 1:
             order = list(rehearse)  # (rank of each rehearsal, in the order run)
@@ -894,7 +885,7 @@ def main():
                 pmc_counters(args.config, kname, variant)
             from sightpy._shard import shard_rows
 
-            npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0, kmax, snake)) * W
+            npix_rank = len(shard_rows(H, max(world, args.shard_of, 1), 0, kmax)) * W
             st_pass = dict(st0[0])
             st_pass["rays_per_depth"] = [r / npass for r in st0[0]["rays_per_depth"]]
             model = kernel_bytes_model(st_pass, spp / npass, npix_rank, sc.camera.lens_radius != 0.0, npass)

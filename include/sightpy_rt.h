@@ -301,10 +301,21 @@ int srt_abi_version(void);
 int srt_device_count(int* count);
 int srt_create(int device, srt_ctx** out);
 int srt_destroy(srt_ctx* ctx);
-/* options: "queue_bytes" (HBM budget for ray queues), "bvh" (0: no triangle BVH), "max_blocks" (grid cap of the wavefront
- * kernels), "pipeline" (1: size every frame slot on each render, so the first pipelined frame
- * allocates nothing), "frame_kernel" (-1 auto = frame kernel for branching scenes, 0 per-depth wavefront
- * kernels, 1 frame kernel), "occupancy" (experiment: waves/SIMD bound of the ex1 variant) */
+/* options (16 keys; unknown keys fail with SRT_ERR_ARG):
+ *   strategy: "frame_kernel" (-1 auto = frame kernel for branching scenes, 0 per-depth wavefront
+ *     kernels, 1 frame kernel), "fuse_primary" (-1 auto, 0/1: single-child paths traced whole in
+ *     k_primary), "chain_rays" (the per-depth path traces whole chains from the first depth with fewer
+ *     rays than this), "bvh" (0: mesh triangles intersected one by one), "collider_seq" (0: no
+ *     straight-line collider-sequence kernel), "sync_lean" (1: synchronous frames run the lean kernel
+ *     too, for measurement), "deterministic" (0: f64 atomics instead of fixed-point sums),
+ *     "pipeline" (1: size every frame slot on each render, so the first pipelined frame allocates
+ *     nothing);
+ *   numpy's stream on the device: "mt_bands" (0: whole-frame stream on every rank), "mt_short" /
+ *     "mt_pipe_split" (band-mode segment lengths, 0: tabulated 2^19-word segments), "mt_gen_nt"
+ *     (generator workgroup, 0 auto / 256 / 320), "mt_jump_parts" (0 auto, 2..8);
+ *   multi-GPU: "shard_bands" (most row bands per rank, 0 auto), "rehearse_shard" ((nranks << 8) |
+ *     rank: act as that rank without a communicator), "rehearse_assemble" (n: rank 0's assembly of an
+ *     n-rank frame rehearsed). */
 int srt_set_option(srt_ctx* ctx, const char* key, int64_t value);
 int srt_upload_scene(srt_ctx* ctx, const srt_scene_desc* scene);
 int srt_render(srt_ctx* ctx, const srt_camera* cam, const srt_render_args* args, srt_stats* stats);

@@ -1462,21 +1462,18 @@ RT_HD void shade_hit(const SceneView& S, int cid, int mi, const Ray& r, double t
 RT_HD uint32_t child_path(uint32_t path, uint32_t slot, uint32_t round) { return mix32(path, slot + 4096u * round); }
 
 // ---- row-band shards of a frame over ranks (SRT_RENDER_SHARDED) ---------------------------------
-// The frame's rows are cut into bands of h rows (the last band shorter), dealt to the n ranks one
-// band per rank per period of n bands (the reference parallelises over samples instead,
-// scene.py:80-116): round-robin (rank q takes band q of every period) or, with `snake`, in
-// alternating direction (odd periods are dealt n-1 .. 0, which cancels a top-to-bottom cost
-// gradient).  A rank's j-th band lies in period j, so its local row i holds a row of period i / h.
-// Interleaving balances the cheap sky rows against the reflective floor rows; each band of a rank
-// is a run of the numpy stream a rank jumps to (~110 us of a CU per jump), so the bands are as tall
-// as the balance allows: h is chosen per (H, n) with at most `kmax` bands per rank (and at least
-// kmax / 2), the fewest rows on the busiest rank first, then the most bands.
+// The frame's rows are cut into bands of h rows (the last band shorter), dealt round-robin to the n
+// ranks, one band per rank per period of n bands (rank q takes band q of every period; the reference
+// parallelises over samples instead, scene.py:80-116).  A rank's j-th band lies in period j, so its
+// local row i holds a row of period i / h.  Interleaving balances the cheap sky rows against the
+// reflective floor rows; each band of a rank is a run of the numpy stream a rank jumps to (~110 us
+// of a CU per jump), so the bands are as tall as the balance allows: h is chosen per (H, n) with at
+// most `kmax` bands per rank (and at least kmax / 2), the fewest rows on the busiest rank first, then
+// the most bands.  (A snake order -- odd periods dealt n-1 .. 0 -- gave the first and the last rank
+// two adjacent bands at every turn, one run of the numpy stream twice as long to generate: ex1 1080p,
+// slowest of 8 ranks 0.317 vs 0.288 ms round-robin, ex4 4K 2.47 vs 2.35 ms,
+// profiles/r03_band_order_ab.txt; removed in round 6.)
 constexpr int SHARD_BANDS = 8;  // kmax: most bands per rank (option "shard_bands"; 0 = shard_kmax's choice)
-// dealing order (option "shard_snake"): round-robin.  A snake deals two adjacent bands to the first
-// and the last rank at every turn, one run of the numpy stream twice as long to generate: ex1 1080p,
-// slowest of 8 ranks 0.317 (snake) vs 0.288 ms (round-robin), ex4 4K 2.47 vs 2.35 ms
-// (profiles/r03_band_order_ab.txt)
-constexpr int SHARD_SNAKE = 0;
 // A Diffuse fan-out scene costs ~50 rays per pixel and sample, so a jump is a fraction of one row's
 // work and the balance wins: bands of SHARD_FANOUT_ROWS rows (cornell 800x800 on 8 ranks, slowest
 // rank of the same frame: 618 ms with 20-row bands, 583 with 4, 570 with 2; profiles/r03_*)
@@ -1489,26 +1486,22 @@ RT_HD int shard_kmax(int64_t H, int n, int kmax_opt, int fanout) {
     }
     return SHARD_BANDS;
 }
-RT_HD int shard_band_owner(int64_t b, int n, int snake) {
-    const int i = (int)(b % n);
-    return (snake && ((b / n) & 1)) ? n - 1 - i : i;
-}
-RT_HD int64_t shard_rank_rows(int64_t H, int n, int q, int64_t h, int snake) {
+RT_HD int shard_band_owner(int64_t b, int n) { return (int)(b % n); }
+RT_HD int64_t shard_rank_rows(int64_t H, int n, int q, int64_t h) {
     const int64_t B = (H + h - 1) / h;  // bands
     const int64_t full = B / n, rem = B % n;
-    int64_t nb = full;  // one band per full period
-    for (int64_t i = 0; i < rem; ++i) nb += shard_band_owner(full * n + i, n, snake) == q;
-    return nb * h - (shard_band_owner(B - 1, n, snake) == q ? B * h - H : 0);
+    const int64_t nb = full + (q < rem ? 1 : 0);  // one band per full period, then bands 0 .. rem-1
+    return nb * h - (shard_band_owner(B - 1, n) == q ? B * h - H : 0);
 }
-RT_HD int64_t shard_max_rows(int64_t H, int n, int64_t h, int snake) {
+RT_HD int64_t shard_max_rows(int64_t H, int n, int64_t h) {
     int64_t m = 0;
     for (int q = 0; q < n; ++q) {
-        const int64_t r = shard_rank_rows(H, n, q, h, snake);
+        const int64_t r = shard_rank_rows(H, n, q, h);
         m = r > m ? r : m;
     }
     return m;
 }
-RT_HD int64_t shard_band_height(int64_t H, int n, int kmax, int snake) {
+RT_HD int64_t shard_band_height(int64_t H, int n, int kmax) {
     if (n <= 1 || H <= 1) return H > 0 ? H : 1;
     if (kmax < 1) kmax = 1;
     int64_t best_h = 1, best_rows = (int64_t)1 << 62;
@@ -1516,12 +1509,12 @@ RT_HD int64_t shard_band_height(int64_t H, int n, int kmax, int snake) {
         int64_t h = (H + (int64_t)n * k - 1) / ((int64_t)n * k);
         if (h < 1) h = 1;
         if ((H + h - 1) / h < n) continue;  // fewer bands than ranks: a rank would get no rows (then h = 1)
-        const int64_t m = shard_max_rows(H, n, h, snake);
+        const int64_t m = shard_max_rows(H, n, h);
         if (m < best_rows) { best_rows = m; best_h = h; }
     }
     return best_h;
 }
-RT_HD int shard_of_row(int64_t y, int n, int64_t h, int snake) { return shard_band_owner(y / h, n, snake); }
+RT_HD int shard_of_row(int64_t y, int n, int64_t h) { return shard_band_owner(y / h, n); }
 RT_HD int64_t shard_local_row(int64_t y, int n, int64_t h) { return (y / (h * n)) * h + y % h; }
 
 // sRGB_linear_to_sRGB + clip + uint8 for one pixel (colour_functions.py:4-18, scene.py:125-140)

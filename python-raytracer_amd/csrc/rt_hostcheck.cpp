@@ -302,12 +302,12 @@ void hc_philox(const uint32_t* ctr, uint32_t k0, uint32_t k1, uint32_t* out) {
 uint32_t hc_mix32(uint32_t h, uint32_t v) { return mix32(h, v); }
 
 // row-band shard map of the sharded render (rt_device.h): band height, owner rank and local row of
-// global row y, with at most kmax bands per rank, round-robin or snake order
+// global row y, with at most kmax bands per rank, dealt round-robin
 int hc_shard_kmax(int64_t H, int n, int kmax, int fanout) { return shard_kmax(H, n, kmax, fanout); }
-int64_t hc_shard_map(int64_t H, int n, int kmax, int snake, int32_t* owner, int64_t* local) {
-    const int64_t h = shard_band_height(H, n, kmax, snake);
+int64_t hc_shard_map(int64_t H, int n, int kmax, int32_t* owner, int64_t* local) {
+    const int64_t h = shard_band_height(H, n, kmax);
     for (int64_t y = 0; y < H; ++y) {
-        owner[y] = shard_of_row(y, n, h, snake);
+        owner[y] = shard_of_row(y, n, h);
         local[y] = shard_local_row(y, n, h);
     }
     return h;

@@ -1005,19 +1005,9 @@ struct Variant {
     void (*lean)(TraceParams) = nullptr;
     void (*lean_stats)(TraceParams) = nullptr;  // k_primary_lean<.., LANE_STATS> (srt_debug_lane_stats)
 };
-// occupancy experiments for the headline scene (srt_set_option "occupancy" = k in 2..4 selects the
-// build for k waves/SIMD, OCC_VARIANTS[k - 2]; built with -DRT_OCC_VARIANTS); the default
-// instantiations use RT_OCC = 3 waves/SIMD.  Same-box A/B
-// against 2 waves/SIMD (profiles/r03_occ_ab.txt): device-resident ex1 1080p 1.22 -> 1.10 ms, ex3
-// k_frame 3.36 -> 3.06 ms, ex4 4K 14.5 -> 13.2 ms, cornell 4.87 -> 4.05 s, mesh 12.2 -> 10.2 ms.
-#ifdef RT_OCC_VARIANTS
-const Variant OCC_VARIANTS[] = {
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 2>, k_trace<MATS_GLOSSY_SKY, 2>, k_frame<MATS_GLOSSY_SKY, 2>, k_trace<MATS_GLOSSY_SKY, 2, true>},
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3>, k_frame<MATS_GLOSSY_SKY, 3>, k_trace<MATS_GLOSSY_SKY, 3, true>},
-    {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4>, k_frame<MATS_GLOSSY_SKY, 4>, k_trace<MATS_GLOSSY_SKY, 4, true>},
-};
-#endif
-int g_occupancy = 0;
+// The trace kernels are built for RT_OCC = 3 waves/SIMD.  Same-box A/B against 2 waves/SIMD
+// (profiles/r03_occ_ab.txt): device-resident ex1 1080p 1.22 -> 1.10 ms, ex3 k_frame 3.36 -> 3.06 ms,
+// ex4 4K 14.5 -> 13.2 ms, cornell 4.87 -> 4.05 s, mesh 12.2 -> 10.2 ms.
 #ifndef RT_OCC
 #define RT_OCC 3
 #endif
@@ -1070,9 +1060,6 @@ const Variant SEQ_VARIANTS[] = {
 };
 #endif
 const Variant& pick_variant(uint32_t mats, uint32_t seq = 0) {
-#ifdef RT_OCC_VARIANTS
-    if (g_occupancy >= 2 && g_occupancy <= 4 && (MATS_GLOSSY_SKY & mats) == mats) return OCC_VARIANTS[g_occupancy - 2];
-#endif
 #ifdef RT_SEQ_VARIANTS
     if (seq)
         for (const Variant& v : SEQ_VARIANTS)
@@ -1280,12 +1267,12 @@ struct GatherTiles {
     int64_t npix[MAX_RANKS];       // rows_q * W
 };
 
-__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t band, int snake, int64_t W,
+__global__ __launch_bounds__(BLOCK) void k_assemble(GatherTiles T, int nranks, int64_t band, int64_t W,
                                                    int64_t H, uint8_t* u8, double* rgb) {
     const int64_t n = W * H;
     for (int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x; g < n; g += (int64_t)gridDim.x * BLOCK) {
         const int64_t y = g / W, x = g - y * W;
-        const int q = shard_of_row(y, nranks, band, snake);
+        const int q = shard_of_row(y, nranks, band);
         const int64_t l = shard_local_row(y, nranks, band) * W + x;
         if (u8) {
             const uint8_t* s = T.u8[q] + 3 * l;
@@ -1306,10 +1293,10 @@ __global__ __launch_bounds__(BLOCK) void k_rgbx(const uint8_t* rgb, uint32_t* rg
         rgbx[i] = (uint32_t)rgb[3 * i] | ((uint32_t)rgb[3 * i + 1] << 8) | ((uint32_t)rgb[3 * i + 2] << 16) | 0xFF000000u;
 }
 
-std::vector<int32_t> band_rows(int64_t H, int n, int q, int64_t band, int snake) {
+std::vector<int32_t> band_rows(int64_t H, int n, int q, int64_t band) {
     std::vector<int32_t> r;
     for (int64_t y = 0; y < H; ++y)
-        if (shard_of_row(y, n, band, snake) == q) r.push_back((int32_t)y);
+        if (shard_of_row(y, n, band) == q) r.push_back((int32_t)y);
     return r;
 }
 
@@ -1377,14 +1364,11 @@ constexpr int MAX_FRAME_SLOTS = 8;
 // (SRT_RENDER_ASYNC) frames rotate over the slots, each with its own stream, so one frame's
 // low-occupancy tail (deep depths, resolve) overlaps the next frame's primary kernel.  Measured on
 // ex1 1080p (ms/frame, device-resident): 1 slot 1.47, 2 slots 1.308, 3 slots 1.292; 1/8 shard 0.28 /
-// 0.202 / 0.199.  The slot count, the generation stream and a separate copy stream are options
-// (srt_set_option "slots", "mt_stream", "copy_stream"): HIP gives a process four hardware queues by
-// default, and a stream that shares a queue with another waits behind that stream's work.
+// 0.202 / 0.199.  HIP gives a process four hardware queues by default, and a stream that shares a
+// queue with another waits behind that stream's work: the slot count follows the queues
+// (default_slots), and host outputs are copied on the frame's own stream.
 struct FrameSlot {
     hipStream_t stream = nullptr;
-    hipEvent_t resolved = nullptr;   // recorded on `stream` after the frame's outputs are final
-    hipEvent_t copied = nullptr;     // recorded on the copy stream after their host copies
-    bool copy_pending = false;       // `copied` guards rgb / u8 of this slot
     hipEvent_t jit_ready = nullptr;  // recorded on the MT stream after this slot's jitter is generated
     hipEvent_t jit_free = nullptr;   // recorded on `stream` after the last kernel that reads the jitter
     hipEvent_t mt_jumped = nullptr;  // recorded on the MT stream after this slot's jump kernel
@@ -1435,7 +1419,6 @@ struct FrameSlot {
     struct Gather {
         bool on = false;
         int64_t W = 0, H = 0, npix = 0, maxpix = 0, band = 1;
-        int snake = 0;
         bool want_u8 = false, want_rgb = false;
         uint8_t* dst_u8 = nullptr;  // where k_assemble writes (caller's device buffer or full_u8)
         double* dst_rgb = nullptr;
@@ -1454,7 +1437,7 @@ struct srt_ctx {
     int device = 0;
     int max_blocks = 2048;
     int ncu = 256;
-    int64_t queue_budget = (int64_t)96 << 30;  // bytes for both ray queues
+    static constexpr int64_t queue_budget = (int64_t)96 << 30;  // bytes for both ray queues
     // scene
     bool has_scene = false;
     SceneView S{};
@@ -1471,8 +1454,6 @@ struct srt_ctx {
     int64_t texel_bytes = 0;
     uint64_t texel_layout = 0;  // hash of the pool layout the records' offsets were remapped to
     bool texels_rgbx = false;  // the resident pool holds 3-channel images as RGBX
-    bool texel_rgbx = true;    // option "texel_rgbx": store 3-channel images as RGBX (one dword per texel)
-    bool sky_prefetch = true;  // option "sky_prefetch" (next srt_upload_scene): trace_one's early sky texel fetch
     // option "mt_jump_parts": blocks per jump window (0: mt_jump_parts's choice)
     int mt_parts_opt = 0;
     // camera tables (shared by the slots; uploaded only when they change)
@@ -1505,9 +1486,6 @@ struct srt_ctx {
     // frame's latency: 2^19-word tabulated segments 0.42 ms, 2^17-word ones ~0.1 ms for 4x the jumps,
     // made in band mode (host jump polynomials, cached per frame shape); 0: tabulated segments
     int64_t mt_short = 65536;
-    // option "mt_short_all": pipelined whole frames take the short segments too (their generation's
-    // latency, not only the first frame's, then shrinks, for four times the jumps)
-    bool mt_short_all = false;
     // option "mt_pipe_split": doubles per band-mode segment of a pipelined whole frame behind others in
     // flight (0: the tabulated 2^19-word segments).  Band mode generates exactly the stored planes' runs
     // (a tabulated segment straddling a stored and a skipped plane generates both), each run cut at the
@@ -1530,9 +1508,10 @@ struct srt_ctx {
     int64_t hint[SRT_MAX_DEPTHS] = {};
     // frame slots; `f` is the one the current call works on
     FrameSlot slots[MAX_FRAME_SLOTS];
-    // pipelined frames: slots they rotate over (option "slots"); the numpy-stream generation of
-    // single-pass frames on a stream of its own ("mt_stream"); host-output copies on a stream of
-    // their own ("copy_stream").  ex1 1080p, host outputs, one MI355X, ms/frame: 3 slots 1.83; 2 slots
+    // pipelined frames: slots they rotate over; the numpy-stream generation of single-pass frames on a
+    // stream of its own (round 2-3 options "slots", "mt_stream", "copy_stream", removed in round 6: the
+    // host-output copies on a stream of their own did not pay).  ex1 1080p, host outputs, one MI355X,
+    // ms/frame: 3 slots 1.83; 2 slots
     // + copy stream 1.83; 3 slots + MT stream 1.82; 2 slots 2.20; 2 slots + MT stream 2.00; one rank's
     // shard of an 8-GPU frame (bench --shard-of 8, same box): 3 slots 0.627, 4 slots 0.544, 3 slots +
     // MT stream 0.857.  Default (default_slots): one slot per hardware queue HIP gives the process
@@ -1540,24 +1519,14 @@ struct srt_ctx {
     // slowest rank 0.318 -> 0.265 ms per frame, the whole ex1 frame 1.30 -> 1.26 ms (8 slots: 0.41 /
     // 1.28; profiles/r03_slots_ab.txt)
     int nslots = 4;
-    // -1 auto: a high-priority stream of its own for whole frames (ex1 1080p 1.80 -> 1.64 ms/frame, same
-    // box), the frame's stream for shards (round 4, same box: one rank of 2 0.87 ms on a stream of its
-    // own, 0.67 on a high-priority one, 0.55 on the frame's stream; of 4 0.33 / 0.48 / 0.32; of 8
-    // 0.20 / 0.33 / 0.21, profiles/r04_mt_stream_ab.txt); 0 the frame's stream; 1 a stream of its own;
-    // 2 a high-priority one
-    int use_mt_stream = -1;
-    // option "mt_gen_stream": where the generators of a whole pipelined frame run when its jump kernel
-    // makes the next frame's key (frame-end jump).  0: after the jump kernel on the MT stream (frame
-    // k+1's jumps then wait behind frame k's generators: the chain jump + generators, ~1 ms under
-    // load, paces the frames); 1: on the frame's own stream (normal priority); 2: on two
-    // high-priority generator streams taken in turn, so the MT stream carries only the jump chain
-    // and consecutive frames' generators overlap
-    // (same box, ex1 1080p pipelined frames, ms: 0 0.940, 1 ~1.05, 2 1.014-1.028 with seven hardware
-    // queues, 0.95-0.96 with nine; profiles/r05_mt_generator_ab.txt)
-    int mt_gen_stream = 0;
-    hipStream_t gen_streams[2] = {nullptr, nullptr};
-    int gen_next = 0;
-    bool use_copy_stream = false;
+    // where the numpy-stream generation runs: a high-priority stream of its own for whole frames (ex1
+    // 1080p 1.80 -> 1.64 ms/frame, same box), the frame's stream for shards (round 4, same box: one
+    // rank of 2 0.87 ms on a stream of its own, 0.67 on a high-priority one, 0.55 on the frame's
+    // stream; of 4 0.33 / 0.48 / 0.32; of 8 0.20 / 0.33 / 0.21, profiles/r04_mt_stream_ab.txt).  The
+    // generators of a whole pipelined frame run after its jump kernel on that stream (frame k+1's
+    // jumps then wait behind frame k's generators); on the frame's own stream or on two high-priority
+    // generator streams taken in turn (round-5 option "mt_gen_stream", removed in round 6) pipelined
+    // ex1 frames took ~1.05 and 1.014-1.028 ms against 0.940 (profiles/r05_mt_generator_ab.txt).
     // option "deterministic" (default 1): contributions added to a pixel by other threads go into
     // order-independent fixed-point sums (bit-reproducible frames); 0: f64 atomics
     bool deterministic = true;
@@ -1582,7 +1551,6 @@ struct srt_ctx {
     // single-pass frames generate their numpy stream on a stream of their own, so the generation of
     // frame k+1 runs beside frame k's trace (their order is this stream's order)
     hipStream_t mt_stream = nullptr;
-    hipStream_t copy_stream = nullptr;  // option copy_stream: the host-output copies of pipelined frames
     bool mt_tables = false;
     // multi-GPU (srt_comm_init / srt_comm_init_all)
     ncclComm_t comm = nullptr;
@@ -1590,24 +1558,20 @@ struct srt_ctx {
     bool defer_gather = false;  // srt_render_group posts the gathers of all its contexts in one group
     bool retry_frame = false;   // the last finish_async failed only with RETRY_* bits (render the frame again)
     int shard_bands = 0;  // option "shard_bands": most row bands per rank (0: rt_device.h shard_kmax by the scene's fan-out)
-    int shard_snake = SHARD_SNAKE;  // option "shard_snake": bands dealt in alternating direction per period
-    int frame_groups = 0;           // option "frame_groups": k_frame sample groups per tile (0: auto)
     // option "fuse_primary": single-child scenes traced whole-path per pixel in k_primary (same image
     // bit for bit as the per-depth kernels); -1 (default) for frames of at least two resident
     // rounds of threads: ex1 1080p 1.308 -> 1.209 ms per frame, a rank of 4 0.47 -> 0.44, while a rank
     // of 8 (1.3 rounds) is faster per depth, 0.29 vs 0.35 (profiles/r03_fused_ab.txt)
     int fuse_primary = -1;
-    int pix_groups_opt = 0;     // option "pix_groups": k_primary's sample groups per pixel (power of two; 0 auto)
     // option "rehearse_assemble" = n (diagnostic, one GPU): a frame rendering rank 0's rows of an
     // n-rank job (rows given, not SRT_RENDER_SHARDED) also does rank 0's assembly -- k_assemble of its
     // tile and n - 1 stand-in tiles of the other ranks' shapes into the whole frame -- and hands back
     // the whole frame's uint8 image (host copy of W x H x 3 bytes), as a sharded rank 0 does after the
     // RCCL gather (the transfers themselves are not rehearsed)
     int rehearse_assemble = 0;
-    int sync_blocks = 0;  // option "sync_blocks": k_primary's grid cap in synchronous frames (0: one block per 256 threads)
-    int lean_blocks = 0;  // option "lean_blocks": grid of k_primary_lean in pipelined frames (0: max_blocks; set to 2 per CU)
-    // option "lean_blocks_shard": the same for a shard's rows (0: max_blocks; set to 4 per CU: every rank of 4
-    // rehearsed, slowest 0.321 -> 0.275 ms per frame; of 8 unchanged, profiles/r05_lean_grid_ab.txt)
+    int lean_blocks = 0;  // grid of k_primary_lean in pipelined whole frames (set to 2 blocks per CU)
+    // the same for a shard's rows (set to 4 per CU: every rank of 4 rehearsed, slowest 0.321 -> 0.275 ms
+    // per frame; of 8 unchanged, profiles/r05_lean_grid_ab.txt)
     int lean_blocks_shard = 0;
     bool sync_lean = false;     // option "sync_lean": synchronous frames run k_primary_lean too (measurement)
     int64_t lean_launches = 0;  // (srt_debug_lean_launches)
@@ -1801,7 +1765,6 @@ int64_t fused_items(const srt_ctx* c) { return 2 * (int64_t)c->ncu * 4 * OCC * 6
 // k_primary's sample groups per pixel (TraceParams::pix_groups): the fewest (a power of two, at most
 // the pass's samples and 64) that give the pass enough threads
 int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
-    if (c->pix_groups_opt > 0) return std::min(c->pix_groups_opt, 64);  // (option "pix_groups": experiments)
     const int64_t want = fused ? fused_items(c) : (int64_t)c->max_blocks * 64;
     int g = 1;
     while (g * 2 <= std::min(ns, 64) && npix * g < want) g *= 2;
@@ -2231,8 +2194,6 @@ int ensure_slot(FrameSlot& f) {
     if (f.stream) return SRT_OK;
     HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&f.jit_ready, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&f.resolved, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&f.copied, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f.jit_free, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f.mt_jumped, hipEventDisableTiming));
     HIP_TRY(dalloc(&f.counts, SRT_MAX_DEPTHS * NSHARD));
@@ -2254,8 +2215,6 @@ void free_slot(FrameSlot& f) {
     for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     if (f.host) (void)hipHostFree(f.host);
     (void)hipEventDestroy(f.jit_ready);
-    (void)hipEventDestroy(f.resolved);
-    (void)hipEventDestroy(f.copied);
     (void)hipEventDestroy(f.jit_free);
     (void)hipEventDestroy(f.mt_jumped);
     (void)hipStreamDestroy(f.stream);
@@ -2273,11 +2232,7 @@ int finish_async(srt_ctx* c, srt_stats* st) {
         return SRT_OK;
     }
     for (FrameSlot& f : c->slots)
-        if (f.stream) {
-            HIP_TRY(hipStreamSynchronize(f.stream));
-            f.copy_pending = false;
-        }
-    if (c->copy_stream) HIP_TRY(hipStreamSynchronize(c->copy_stream));
+        if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
     c->async_pending = 0;
     if (c->mt_chain) {  // numpy's state after the last asynchronous frame's draws
         HIP_TRY(hipMemcpy(c->mt_chain->key, mt_dump(c), rtmt::N * 4, hipMemcpyDeviceToHost));
@@ -2321,7 +2276,7 @@ int finish_async(srt_ctx* c, srt_stats* st) {
 }
 
 int64_t shard_npix(const FrameSlot::Gather& G, int nranks, int q) {
-    return shard_rank_rows(G.H, nranks, q, G.band, G.snake) * G.W;
+    return shard_rank_rows(G.H, nranks, q, G.band) * G.W;
 }
 
 // Post this rank's part of the frame's gather on its stream (inside an RCCL group): rank 0 receives
@@ -2368,7 +2323,7 @@ int gather_finish(srt_ctx* c) {
         T.npix[q] = shard_npix(G, c->nranks, q);
     }
     hipStream_t st = c->f->stream;
-    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.band, G.snake, G.W, G.H,
+    hipLaunchKernelGGL(k_assemble, dim3(grid_for(G.W * G.H, c->max_blocks)), dim3(BLOCK), 0, st, T, c->nranks, G.band, G.W, G.H,
                        G.want_u8 ? G.dst_u8 : nullptr, G.want_rgb ? G.dst_rgb : nullptr);
     HIP_TRY(hipGetLastError());
     if (G.host_u8) HIP_TRY(hipMemcpyAsync(G.host_u8, G.dst_u8, (size_t)3 * G.W * G.H, hipMemcpyDeviceToHost, st));
@@ -2439,9 +2394,6 @@ int srt_destroy(srt_ctx* c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->mt_done) (void)hipEventDestroy(c->mt_done);
     if (c->mt_stream) (void)hipStreamDestroy(c->mt_stream);
-    for (hipStream_t g : c->gen_streams)
-        if (g) (void)hipStreamDestroy(g);
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     void* bufs[] = {c->xs, c->ys, c->rows, c->mt, c->mt_out, c->texels, c->red, c->mt_y, c->lane_stats};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -2457,18 +2409,10 @@ int srt_destroy(srt_ctx* c) {
 int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return fail(SRT_ERR_ARG, "null ctx/key");
     c->pf.valid = false;  // (an option may change the streams or the generation a prefetch assumed)
-    if (!strcmp(key, "queue_bytes")) { c->queue_budget = value; return SRT_OK; }
-    if (!strcmp(key, "occupancy")) { g_occupancy = (int)value; return SRT_OK; }
     if (!strcmp(key, "pipeline")) { c->pipeline = value != 0; return SRT_OK; }
     if (!strcmp(key, "bvh")) { c->use_bvh = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_bands")) { c->mt_bands_on = value != 0; return SRT_OK; }
-    if (!strcmp(key, "mt_gen_stream")) {
-        if (value < 0 || value > 2) return fail(SRT_ERR_ARG, "mt_gen_stream: 0, 1 or 2");
-        c->mt_gen_stream = (int)value;
-        return SRT_OK;
-    }
     if (!strcmp(key, "collider_seq")) { c->seq_on = value != 0; return SRT_OK; }
-    if (!strcmp(key, "mt_short_all")) { c->mt_short_all = value != 0; return SRT_OK; }
     if (!strcmp(key, "mt_pipe_split")) {
         if (value != 0 && (value < 4096 || value > ((int64_t)1 << 24)))
             return fail(SRT_ERR_ARG, "mt_pipe_split: 0 or 4096 .. 2^24 doubles");
@@ -2481,21 +2425,6 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         return SRT_OK;
     }
     if (!strcmp(key, "sync_lean")) { c->sync_lean = value != 0; return SRT_OK; }
-    if (!strcmp(key, "lean_blocks_shard")) {
-        if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "lean_blocks_shard: 0 (max_blocks) or a grid size");
-        c->lean_blocks_shard = (int)value;
-        return SRT_OK;
-    }
-    if (!strcmp(key, "lean_blocks")) {
-        if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "lean_blocks: 0 (max_blocks) or a grid size");
-        c->lean_blocks = (int)value;
-        return SRT_OK;
-    }
-    if (!strcmp(key, "sync_blocks")) {
-        if (value < 0 || value > INT_MAX) return fail(SRT_ERR_ARG, "sync_blocks: 0 (one block per 256 threads) or a grid cap");
-        c->sync_blocks = (int)value;
-        return SRT_OK;
-    }
     if (!strcmp(key, "rehearse_assemble")) {
         if (value != 0 && (value < 2 || value > MAX_RANKS)) return fail(SRT_ERR_ARG, "rehearse_assemble: 0 or 2 .. 64");
         c->rehearse_assemble = (int)value;
@@ -2506,21 +2435,10 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         c->mt_short = value;
         return SRT_OK;
     }
-    if (!strcmp(key, "texel_rgbx")) { c->texel_rgbx = value != 0; return SRT_OK; }  // (next srt_upload_scene)
-    if (!strcmp(key, "sky_prefetch")) { c->sky_prefetch = value != 0; return SRT_OK; }  // (next srt_upload_scene)
     if (!strcmp(key, "mt_jump_parts")) {
         if (value != 0 && (value < MT_MIN_PARTS || value > MT_MAX_PARTS))
             return fail(SRT_ERR_ARG, "mt_jump_parts: 0 (auto) or 2 .. 8");
         c->mt_parts_opt = (int)value;
-        return SRT_OK;
-    }
-    if (!strcmp(key, "frame_groups")) {
-        if (value < 0 || value > 4096) return fail(SRT_ERR_ARG, "frame_groups: 0 (auto) .. 4096");
-        c->frame_groups = (int)value;
-        return SRT_OK;
-    }
-    if (!strcmp(key, "shard_snake")) {
-        c->shard_snake = value != 0;
         return SRT_OK;
     }
     if (!strcmp(key, "shard_bands")) {
@@ -2530,13 +2448,7 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
     }
     if (!strcmp(key, "chain_rays")) { c->chain_rays = value; return SRT_OK; }
     if (!strcmp(key, "fuse_primary")) { c->fuse_primary = (int)value; return SRT_OK; }
-    if (!strcmp(key, "pix_groups")) {
-        if (value < 0 || value > 64 || (value & (value - 1))) return fail(SRT_ERR_ARG, "pix_groups: 0 (auto) or 1, 2, 4 .. 64");
-        c->pix_groups_opt = (int)value;
-        return SRT_OK;
-    }
     if (!strcmp(key, "frame_kernel")) { c->use_frame = value < 0 ? -1 : (value != 0); return SRT_OK; }
-    if (!strcmp(key, "max_blocks")) { c->max_blocks = (int)std::max<int64_t>(NSHARD, value); return SRT_OK; }
     if (!strcmp(key, "deterministic")) {
         HIP_TRY(hipSetDevice(c->device));
         int rc = finish_async(c, nullptr);
@@ -2556,25 +2468,6 @@ int srt_set_option(srt_ctx* c, const char* key, int64_t value) {
         if (rc) return rc;
         c->nranks = n;
         c->rank = r;
-        return SRT_OK;
-    }
-    if (!strcmp(key, "slots") || !strcmp(key, "mt_stream") || !strcmp(key, "copy_stream")) {
-        if (!strcmp(key, "slots") && (value < 1 || value > MAX_FRAME_SLOTS)) return fail(SRT_ERR_ARG, "slots: 1..8");
-        HIP_TRY(hipSetDevice(c->device));
-        int rc = finish_async(c, nullptr);  // the frames in flight finish on the old arrangement
-        if (rc) return rc;
-        if (!strcmp(key, "slots")) {
-            c->nslots = (int)value;
-            c->next_slot = 0;
-        } else if (!strcmp(key, "mt_stream")) {
-            c->use_mt_stream = (int)std::min<int64_t>(std::max<int64_t>(value, -1), 2);
-            if (c->mt_stream) {
-                (void)hipStreamDestroy(c->mt_stream);
-                c->mt_stream = nullptr;
-            }
-        } else {
-            c->use_copy_stream = value != 0;
-        }
         return SRT_OK;
     }
     return fail(SRT_ERR_ARG, std::string("unknown option ") + key);
@@ -2633,7 +2526,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     // dword load (texel_rgb) instead of three byte loads; the records point into that layout
     std::vector<srt_texture> tex_h(d->textures, d->textures + std::max(0, d->n_textures));
     std::vector<std::array<int64_t, 4>> imgs;  // (offset, bytes, new offset, expand) per image
-    bool rgbx = c->texel_rgbx && d->texel_bytes > 0 && d->texels && !is_device_ptr(d->texels);
+    bool rgbx = d->texel_bytes > 0 && d->texels && !is_device_ptr(d->texels);
     if (rgbx) {
         for (const srt_texture& t : tex_h) {
             const int64_t bytes = (int64_t)t.height * t.width * t.channels;
@@ -2718,7 +2611,7 @@ int srt_upload_scene(srt_ctx* c, const srt_scene_desc* d) {
     S.light_local = (decltype(S.light_local))ll; S.importance = (decltype(S.importance))imp;
     S.ncol = d->n_colliders; S.nmat = d->n_materials; S.ntex = d->n_textures; S.nlights = d->n_lights;
     S.nmedia = d->n_media; S.nimp = d->n_importance;
-    S.sky_col = c->sky_prefetch ? sky_collider(d->colliders, d->n_colliders, d->materials) : -1;
+    S.sky_col = sky_collider(d->colliders, d->n_colliders, d->materials);
     S.nshadow = 0;
     bool lin_tri = false;
     {
@@ -2816,9 +2709,8 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
         if (c->nranks > MAX_RANKS) return fail(SRT_ERR_ARG, "too many ranks");
         if (cam->height < c->nranks) return fail(SRT_ERR_ARG, "a sharded frame needs at least one row per rank");
         if (a->out_hit_id) return fail(SRT_ERR_ARG, "hit ids of a sharded frame are not gathered");
-        band = shard_band_height(cam->height, c->nranks, shard_kmax(cam->height, c->nranks, c->shard_bands, c->fanout),
-                                 c->shard_snake);
-        rows_h = band_rows(cam->height, c->nranks, c->rank, band, c->shard_snake);
+        band = shard_band_height(cam->height, c->nranks, shard_kmax(cam->height, c->nranks, c->shard_bands, c->fanout));
+        rows_h = band_rows(cam->height, c->nranks, c->rank, band);
         n_rows = (int)rows_h.size();
         if (n_rows == 0) return fail(SRT_ERR_ARG, "a sharded frame left this rank without rows");
         rows_src = rows_h.data();
@@ -2881,7 +2773,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
         // into groups, one block per (tile, group), until there are ~4 blocks per resident wave
         // slot (c->max_blocks = 4 OCC per CU)
         const int64_t want = 4 * (int64_t)c->max_blocks;
-        const int64_t g = c->frame_groups > 0 ? c->frame_groups : (want + ntiles - 1) / ntiles;
+        const int64_t g = (want + ntiles - 1) / ntiles;
         F.groups = (int)std::max<int64_t>(1, std::min<int64_t>(g, batch));
     }
     // fused paths (single-child scenes): by default when the frame's threads (sample groups
@@ -2924,7 +2816,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
     // band mode (srt_ctx::mt_short); later pipelined frames generate behind their predecessors in
     // band-mode segments of mt_pipe_split doubles (0: the tabulated 2^19-word segments)
     const int64_t whole_split = n_rows < Hf ? 0
-                              : (c->async_pending == 0 || c->mt_short_all) ? c->mt_short
+                              : c->async_pending == 0 ? c->mt_short
                                                                            : c->mt_pipe_split;
     if (use_mt && c->mt_bands_on && (n_rows < Hf || whole_split > 0)) {
         const int last_ns = a->spp - (F.npass - 1) * batch;
@@ -2944,18 +2836,18 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
                              (F.npass == 1 || rtmt::end_jump(pass_words(batch, false)) > 0);
     const int64_t jit_doubles = use_mt ? (int64_t)batch * 4 * (jit_compact ? npix : W * Hf)
                                        : (a->jitter && !jit_dev ? (int64_t)batch * 4 * npix : 0);
-    const int64_t maxpix = sharded ? shard_max_rows(Hf, c->nranks, band, c->shard_snake) * W : 0;  // the gather's tile
+    const int64_t maxpix = sharded ? shard_max_rows(Hf, c->nranks, band) * W : 0;  // the gather's tile
     // rank 0's assembly rehearsed (srt_ctx::rehearse_assemble): these rows are rank 0's of an n-rank job
     int reh_n = 0;
     int64_t reh_band = 1, reh_maxpix = 0;
     if (c->rehearse_assemble > 1 && !sharded && a->rows && a->out_srgb8 && ptr_kind(a->out_srgb8) != 1 &&
         !(a->flags & SRT_RENDER_RGBX)) {
         const int n = c->rehearse_assemble;
-        reh_band = shard_band_height(Hf, n, shard_kmax(Hf, n, c->shard_bands, c->fanout), c->shard_snake);
-        const std::vector<int32_t> r0 = band_rows(Hf, n, 0, reh_band, c->shard_snake);
+        reh_band = shard_band_height(Hf, n, shard_kmax(Hf, n, c->shard_bands, c->fanout));
+        const std::vector<int32_t> r0 = band_rows(Hf, n, 0, reh_band);
         if ((int)r0.size() == n_rows && std::equal(r0.begin(), r0.end(), rows_src)) {
             reh_n = n;
-            reh_maxpix = shard_max_rows(Hf, n, reh_band, c->shard_snake) * W;
+            reh_maxpix = shard_max_rows(Hf, n, reh_band) * W;
         }
     }
     // frames in flight use the buffers below: a frame that would reallocate anything first waits
@@ -3085,7 +2977,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
                                  : ((async && F.fuse && pick_variant(c->mats, c->seq_on ? c->seq : 0).lean != nullptr) ? 256
                                                                                                           : rtmt_dev::MT_GEN_THREADS);
     bool pf_hit = false;
-    const int mts = use_mt ? (c->use_mt_stream >= 0 ? c->use_mt_stream : (n_rows >= Hf ? 2 : 0)) : 0;
+    const int mts = use_mt ? (n_rows >= Hf ? 2 : 0) : 0;
     const int64_t pf_shape[8] = {W, Hf, a->spp, batch, mt_pm, (int64_t)(c->f - c->slots), mts,
                                  (int64_t)c->mt_bands_on * 2 + (c->mt_short > 0)};
     if (prefetch && (F.npass != 1 || !mts)) return SRT_OK;  // (the generation would run on the frame's stream)
@@ -3178,19 +3070,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
                 const uint32_t* end_poly = nullptr;
                 if (end && (rc = mt_end_poly_for(c, n_words, &end_poly))) return rc;
                 // (a pinhole camera reads only the pixel-jitter planes 0 and 1 of each sample)
-                // (a pipelined whole frame's generators off the jump chain: see srt_ctx::mt_gen_stream)
-                hipStream_t gst = mst;
-                if (mst != c->f->stream && end && c->mt_gen_stream == 1) gst = c->f->stream;
-                if (mst != c->f->stream && end && c->mt_gen_stream == 2) {
-                    hipStream_t& g = c->gen_streams[c->gen_next];
-                    if (!g) {
-                        int lo = 0, hi = 0;
-                        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                        HIP_TRY(hipStreamCreateWithPriority(&g, hipStreamNonBlocking, hi));
-                    }
-                    gst = g;
-                    c->gen_next ^= 1;
-                }
+                const hipStream_t gst = mst;
                 hipStream_t gen_on = mst;
                 if (pf_hit && p == 0) {  // queued by srt_render_prefetch
                     mt_pos = pf_in.final_pos;
@@ -3258,8 +3138,6 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
                 P.out_rgb = res_rgb;
                 P.out_u8 = res_u8;
                 P.spp_total = a->spp;
-                // (the fused resolve rewrites rgb / u8: the previous frame's copies from them first)
-                if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
                 HIP_TRY(hipEventRecord(ev[0], c->f->stream));
                 hipLaunchKernelGGL(V.frame, dim3((unsigned)(ntiles * P.groups)), dim3(FRAME_BLOCK), lut_bytes(c),
                                    c->f->stream, P);
@@ -3288,7 +3166,6 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             P.out_rgb = res_rgb;
             P.out_u8 = res_u8;
             P.spp_total = a->spp;
-            if (P.fuse_resolve && c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
             // grid: frames in flight overlap one frame's tail with the next, and fewer, longer blocks
             // (grid-stride, max_blocks: four rounds of the resident blocks) leave the numpy-stream
             // generators of the frames behind more room; a synchronous frame has nothing to overlap,
@@ -3298,14 +3175,14 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             // the lean kernel of pipelined whole frames (its generators beside it): two blocks per CU,
             // each grid-striding over ~30 wave iterations of a 1080p frame; the frames in flight fill
             // the rest of the CU (ex1 1080p: 0.878 ms per frame at 3072 blocks, 0.838 at 512; a rank of
-            // 8's shard, 2025 blocks at most, was slower with it: profiles/r05_lean_grid_ab.txt; option
-            // lean_blocks).  A pipeline's first frame, with nothing in flight to fill the CUs around its
-            // blocks, keeps the full four rounds (max_blocks).
+            // 8's shard, 2025 blocks at most, was slower with it: profiles/r05_lean_grid_ab.txt).  A
+            // pipeline's first frame, with nothing in flight to fill the CUs around its blocks, keeps
+            // the full four rounds (max_blocks).
             // (option sync_lean: synchronous frames take the lean kernel too -- bench.py times the pipelined
             // frames' kernel alone that way for its roofline)
             const bool lean = F.fuse && (async || c->sync_lean) && V.lean;
             if (lean) c->lean_launches++;
-            const int pgrid = !async ? (c->sync_blocks > 0 ? c->sync_blocks : INT_MAX)
+            const int pgrid = !async ? INT_MAX
                                      : (!lean || c->async_pending == 0               ? c->max_blocks
                                         : n_rows == Hf && c->lean_blocks > 0              ? c->lean_blocks
                                         : n_rows < Hf && c->lean_blocks_shard > 0         ? c->lean_blocks_shard
@@ -3356,7 +3233,6 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
         // the counters and the shadow count)
         const bool fused = F.npass == 1 && ((F.frame && F.groups == 1) || F.fuse);
         uint32_t* hlast = c->f->host + (F.npass - 1) * F.pass_words;
-        if (c->f->copy_pending) HIP_TRY(hipStreamWaitEvent(c->f->stream, c->f->copied, 0));
         hipLaunchKernelGGL(k_resolve, dim3(fused ? 1 : grid_for(npix, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, c->f->fb,
                            (F.frame || !c->deterministic || !c->fx_ok) ? nullptr
                                                                        : (const unsigned long long*)c->f->fbx,
@@ -3364,28 +3240,21 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
                            used_words, c->f->flags, hlast, hlast + F.cnt_words);
         HIP_TRY(hipGetLastError());
         c->f->dirty = false;  // the kernels above leave counts/flags/shadow zeroed
-        // this rank's rows of the linear RGB into the shared host frame: per plane and per class of
-        // bands with one frame-row stride (round-robin: all of them, a rank's band j at frame band
-        // j n + rank; snake: even and odd j), one pitched copy of the full bands, then a short last band
+        // this rank's rows of the linear RGB into the shared host frame: per plane, the rank's band j
+        // at frame band j n + rank, one pitched copy of the full bands, then a short last band
         if (rgb_rows) {
             const int64_t band_px = band * W;
             const int64_t nb = npix / band_px, tail = npix - nb * band_px;
-            const int step = c->shard_snake ? 2 : 1;
             for (int pl = 0; pl < 3; ++pl) {
                 double* dst = a->out_rgb + (int64_t)pl * W * Hf;
                 const double* src = c->f->rgb + (int64_t)pl * npix;
-                for (int cls = 0; cls < step; ++cls) {
-                    const int64_t cnt = nb > cls ? (nb - cls + step - 1) / step : 0;
-                    if (cnt == 0) continue;
-                    const int64_t b0 = (int64_t)cls * c->nranks + (c->shard_snake && (cls & 1) ? c->nranks - 1 - c->rank
-                                                                                                 : c->rank);
-                    HIP_TRY(hipMemcpy2DAsync(dst + b0 * band_px, (size_t)(step * c->nranks * band_px * 8),
-                                             src + cls * band_px, (size_t)(step * band_px * 8), (size_t)(band_px * 8),
-                                             (size_t)cnt, hipMemcpyDeviceToHost, c->f->stream));
-                }
+                if (nb > 0)
+                    HIP_TRY(hipMemcpy2DAsync(dst + (int64_t)c->rank * band_px, (size_t)(c->nranks * band_px * 8), src,
+                                             (size_t)(band_px * 8), (size_t)(band_px * 8), (size_t)nb,
+                                             hipMemcpyDeviceToHost, c->f->stream));
                 if (tail > 0) {
                     // (the rank's band nb, in period nb)
-                    const int64_t bt = nb * c->nranks + ((c->shard_snake && (nb & 1)) ? c->nranks - 1 - c->rank : c->rank);
+                    const int64_t bt = nb * c->nranks + c->rank;
                     HIP_TRY(hipMemcpyAsync(dst + bt * band_px, src + nb * band_px, (size_t)(tail * 8),
                                            hipMemcpyDeviceToHost, c->f->stream));
                 }
@@ -3401,7 +3270,6 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             G.npix = npix;
             G.maxpix = maxpix;
             G.band = band;
-            G.snake = c->shard_snake;
             G.want_u8 = true;
             G.want_rgb = gather_rgb;
             if (c->rank == 0) {
@@ -3417,10 +3285,10 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             GatherTiles T{};
             for (int q = 0; q < reh_n; ++q) {
                 T.u8[q] = q == 0 ? c->f->u8 : c->f->g_u8 + (int64_t)q * reh_maxpix * 3;
-                T.npix[q] = shard_rank_rows(Hf, reh_n, q, reh_band, c->shard_snake) * W;
+                T.npix[q] = shard_rank_rows(Hf, reh_n, q, reh_band) * W;
             }
             hipLaunchKernelGGL(k_assemble, dim3(grid_for(W * Hf, c->max_blocks)), dim3(BLOCK), 0, c->f->stream, T, reh_n,
-                               reh_band, c->shard_snake, W, Hf, c->f->full_u8, (double*)nullptr);
+                               reh_band, W, Hf, c->f->full_u8, (double*)nullptr);
             HIP_TRY(hipGetLastError());
             u8_src = c->f->full_u8;
             u8_bytes = 3 * W * Hf;
@@ -3438,20 +3306,10 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             if (sharded && !c->defer_gather && (rc = gather_frame(c))) return rc;
             if (!sharded && ((a->out_srgb8 && !u8_direct) || (a->out_rgb && !rgb_direct))) {
                 hipStream_t cs = c->f->stream;
-                if (c->use_copy_stream) {
-                    if (!c->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-                    cs = c->copy_stream;
-                    HIP_TRY(hipEventRecord(c->f->resolved, c->f->stream));
-                    HIP_TRY(hipStreamWaitEvent(cs, c->f->resolved, 0));
-                }
                 if (a->out_srgb8 && !u8_direct)
                     HIP_TRY(hipMemcpyAsync(a->out_srgb8, u8_src, (size_t)u8_bytes, hipMemcpyDeviceToHost, cs));
                 if (a->out_rgb && !rgb_direct)
                     HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->rgb, (size_t)3 * npix * 8, hipMemcpyDeviceToHost, cs));
-                if (c->use_copy_stream) {
-                    HIP_TRY(hipEventRecord(c->f->copied, cs));
-                    c->f->copy_pending = true;
-                }
             }
             // host outputs (pinned) are copied on the frame's stream; stats and errors come with
             // srt_render_finish; the next asynchronous frame goes to the next slot
@@ -4254,7 +4112,6 @@ int srt_synchronize(srt_ctx* c) {
     HIP_TRY(hipSetDevice(c->device));
     for (FrameSlot& f : c->slots)
         if (f.stream) HIP_TRY(hipStreamSynchronize(f.stream));
-    if (c->copy_stream) HIP_TRY(hipStreamSynchronize(c->copy_stream));
     return SRT_OK;
 }
 

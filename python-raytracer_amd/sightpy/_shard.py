@@ -5,8 +5,7 @@ callers and tests.
 The reference parallelises `Scene.render` over samples with `multiprocessing.Pool`
 (`sightpy/scene.py:80-116`).  Pixels are independent, so here the frame is split instead: the rows
 are cut into bands of h rows (the last one shorter) and every period of `world` bands is dealt one
-band per rank -- round-robin, or with `snake` in alternating direction (odd periods dealt
-world-1 .. 0, cancelling a top-to-bottom cost gradient).  Interleaving balances the cheap sky rows
+band per rank, round-robin.  Interleaving balances the cheap sky rows
 against the reflective floor rows; every rank renders its rows with the same per-pixel random
 numbers the single-GPU render would use; the library gathers the uint8 (and linear-RGB) tiles to
 rank 0 over RCCL and assembles the frame there.  The image is independent of the number of ranks.
@@ -19,7 +18,6 @@ fan-out scene, whose rows cost ~30x more, takes 2-row bands (shard_kmax).
 import numpy as np
 
 SHARD_BANDS = 8  # kmax (library option "shard_bands"; 0 = shard_kmax's choice)
-SHARD_SNAKE = 0  # dealing order (library option "shard_snake")
 SHARD_FANOUT_ROWS = 2  # band rows of a Diffuse fan-out scene (rt_device.h shard_kmax)
 
 
@@ -49,22 +47,20 @@ def scene_fanout(scene):
     return fan
 
 
-def band_owner(b, world, snake=SHARD_SNAKE):
+def band_owner(b, world):
     """Rank of band `b` (rt_device.h shard_band_owner); b may be an array."""
-    b = np.asarray(b)
-    i = b % world
-    return np.where(np.logical_and(bool(snake), (b // world) % 2 == 1), world - 1 - i, i)
+    return np.asarray(b) % world
 
 
-def rank_rows(height, world, rank, band, snake=SHARD_SNAKE):
+def rank_rows(height, world, rank, band):
     """Rows of `rank` with bands of `band` rows (rt_device.h shard_rank_rows)."""
     B = -(-int(height) // band)
-    owners = band_owner(np.arange(B), world, snake)
+    owners = band_owner(np.arange(B), world)
     nb = int((owners == rank).sum())
     return nb * band - ((B * band - height) if owners[-1] == rank else 0)
 
 
-def band_height(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
+def band_height(height, world, kmax=0, fanout=1):
     """Band height of a `world`-rank frame of `height` rows (rt_device.h shard_band_height)."""
     height = int(height)
     if world <= 1 or height <= 1:
@@ -75,30 +71,30 @@ def band_height(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
         h = max(-(-height // (world * k)), 1)
         if -(-height // h) < world:  # fewer bands than ranks: a rank would get no rows
             continue
-        m = max(rank_rows(height, world, q, h, snake) for q in range(world))
+        m = max(rank_rows(height, world, q, h) for q in range(world))
         if best_rows is None or m < best_rows:
             best_h, best_rows = h, m
     return best_h
 
 
-def shard_rows(height, world, rank, kmax=0, snake=SHARD_SNAKE, fanout=1):
+def shard_rows(height, world, rank, kmax=0, fanout=1):
     """Image rows owned by `rank` (ascending)."""
-    h = band_height(height, world, kmax, snake, fanout)
+    h = band_height(height, world, kmax, fanout)
     rows = np.arange(int(height))
-    return rows[band_owner(rows // h, world, snake) == rank]
+    return rows[band_owner(rows // h, world) == rank]
 
 
-def max_shard_rows(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
+def max_shard_rows(height, world, kmax=0, fanout=1):
     """Largest per-rank row count (the padded tile height of the gather)."""
-    return max(len(shard_rows(height, world, r, kmax, snake, fanout)) for r in range(world))
+    return max(len(shard_rows(height, world, r, kmax, fanout)) for r in range(world))
 
 
-def assemble_index(height, world, kmax=0, snake=SHARD_SNAKE, fanout=1):
+def assemble_index(height, world, kmax=0, fanout=1):
     """For every image row, its position in the gathered buffer of padded tiles:
     `gathered.reshape(world * maxrows, ...)[idx]` is the image."""
-    maxrows = max_shard_rows(height, world, kmax, snake, fanout)
+    maxrows = max_shard_rows(height, world, kmax, fanout)
     idx = np.empty(int(height), dtype=np.int64)
     for r in range(world):
-        rows = shard_rows(height, world, r, kmax, snake, fanout)
+        rows = shard_rows(height, world, r, kmax, fanout)
         idx[rows] = r * maxrows + np.arange(len(rows))
     return idx

@@ -57,40 +57,34 @@ def test_shard_rows_partition():
     assert band_height(800, 8) == 20 and [len(shard_rows(800, 8, r)) for r in range(8)] == [100] * 8
     # one band per rank allowed: contiguous blocks
     assert band_height(1080, 8, kmax=1) == 135
-    # snake order: period 1 is dealt backwards
-    assert list(shard_rows(40, 2, 0, kmax=2, snake=1)) == list(range(0, 10)) + list(range(30, 40))
-    assert list(shard_rows(40, 2, 0, kmax=2, snake=0)) == list(range(0, 10)) + list(range(20, 30))
+    # round-robin: rank 0 takes band 0 of every period
+    assert list(shard_rows(40, 2, 0, kmax=2)) == list(range(0, 10)) + list(range(20, 30))
 
 
-def _kernel_shard_map(H, n, kmax=8, snake=None):
+def _kernel_shard_map(H, n, kmax=8):
     import hostcheck as HC
-    from sightpy._shard import SHARD_SNAKE
-
-    snake = SHARD_SNAKE if snake is None else snake
 
     owner = np.empty(H, dtype=np.int32)
     local = np.empty(H, dtype=np.int64)
     lib = HC.lib()
-    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
-                                 ctypes.c_void_p]
+    lib.hc_shard_map.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     lib.hc_shard_map.restype = ctypes.c_int64
-    h = lib.hc_shard_map(H, n, kmax, snake, owner.ctypes.data, local.ctypes.data)
+    h = lib.hc_shard_map(H, n, kmax, owner.ctypes.data, local.ctypes.data)
     return owner, local, h
 
 
 @pytest.mark.parametrize("H", [8, 9, 13, 37, 300, 800, 1080, 2160])
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
 @pytest.mark.parametrize("kmax", [1, 4, 8, 17])
-@pytest.mark.parametrize("snake", [0, 1])
-def test_kernel_shard_map_matches_partition(H, n, kmax, snake):
+def test_kernel_shard_map_matches_partition(H, n, kmax):
     from sightpy._shard import shard_rows, band_height, rank_rows
 
-    owner, local, h = _kernel_shard_map(H, n, kmax, snake)
-    assert h == band_height(H, n, kmax, snake)
+    owner, local, h = _kernel_shard_map(H, n, kmax)
+    assert h == band_height(H, n, kmax)
     for q in range(n):
-        rows = shard_rows(H, n, q, kmax, snake)
+        rows = shard_rows(H, n, q, kmax)
         assert len(rows) > 0  # (H >= n) every rank gets rows, e.g. H = 9 over 8 ranks with one band each
-        assert len(rows) == rank_rows(H, n, q, h, snake)
+        assert len(rows) == rank_rows(H, n, q, h)
         assert np.array_equal(np.where(owner == q)[0], rows)
         assert np.array_equal(local[rows], np.arange(len(rows)))
         # a rank's j-th band lies in period j (the RGB row copies and the local-row map rely on it)
@@ -110,8 +104,8 @@ def test_kernel_band_count_rule_matches_partition(H, n, kmax, fanout):
     lib.hc_shard_kmax.restype = ctypes.c_int
     k = lib.hc_shard_kmax(H, n, kmax, fanout)
     assert k == shard_kmax(H, n, kmax, fanout)
-    owner, local, h = _kernel_shard_map(H, n, k, 1)
-    assert h == band_height(H, n, kmax, 1, fanout)
+    owner, local, h = _kernel_shard_map(H, n, k)
+    assert h == band_height(H, n, kmax, fanout)
     if fanout > 2 and not kmax and H >= 4 * n * 8:
         assert h <= 4  # k in [kmax / 2, kmax]: at most twice the 2-row bands
 
@@ -353,8 +347,8 @@ def test_gpu_every_shard_of_an_n_rank_frame_assembles_to_the_plain_render(world)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,kmax,snake", [(2, 8, 1), (3, 8, 0), (3, 8, 1), (3, 3, 1), (8, 2, 1), (8, 17, 0)])
-def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax, snake):
+@pytest.mark.parametrize("world,kmax", [(2, 8), (3, 8), (3, 3), (8, 2), (8, 17)])
+def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax):
     """SRT_RENDER_RGB_ROWS (the multi-GPU bench's output path): each rank writes its own rows of the
     linear RGB into one host frame with pitched copies.  Rehearsed on one card (option
     rehearse_shard: act as rank r of N without a communicator): the N shards, rendered in turn into
@@ -363,7 +357,6 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax, snake):
 
     import scenes
     from sightpy import _backend as B, _native as N
-    from sightpy._shard import SHARD_BANDS, SHARD_SNAKE
 
     W, H, spp = 120, 70, 2  # 70 rows: a short last band
     sc = scenes.example1(W, H, 4)
@@ -375,7 +368,6 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax, snake):
     host = ctypes.c_void_p()
     N.check(lib, lib.srt_host_alloc(ctx, 3 * W * H * 8, ctypes.byref(host)))
     N.check(lib, lib.srt_set_option(ctx, b"shard_bands", kmax))
-    N.check(lib, lib.srt_set_option(ctx, b"shard_snake", snake))
     try:
         frame = np.ctypeslib.as_array((ctypes.c_double * (3 * W * H)).from_address(host.value))
         frame[:] = np.nan
@@ -397,7 +389,6 @@ def test_gpu_rgb_rows_shards_fill_the_shared_host_frame(world, kmax, snake):
     finally:
         lib.srt_set_option(ctx, b"rehearse_shard", 0)
         lib.srt_set_option(ctx, b"shard_bands", 0)  # back to the automatic choice
-        lib.srt_set_option(ctx, b"shard_snake", SHARD_SNAKE)
         lib.srt_host_free(ctx, host)
 
 
