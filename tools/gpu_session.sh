@@ -42,7 +42,7 @@ for step in "$@"; do
                 case $C in cornell*) st=2;; example4*) st=10;; *) st=100;; esac
                 run "whole_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup $((st > 50 ? 300 : 2))
                 for n in ${SHARD_NS:-2 4 8}; do
-                  run "shard${n}_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup 2 --shard-of $n --shard-rank all
+                  run "shard${n}_$C" 300 python3 bench.py --config $C --no-cpu-baseline --no-secondary --steps $st --warmup 2 --shard-of $n --shard-rank all ${SHARD_ARGS:-}
                 done
               done ;;
     mttests) run mttests 600 python3 -u -m pytest tests/test_multirank.py tests/test_mt.py tests/test_gpu.py -x -v -m gpu -k "band or shard or mt or numpy_stream or async" --timeout 300 --timeout-method thread -rf ;;
