@@ -1053,10 +1053,21 @@ constexpr uint32_t seq_bits(std::initializer_list<int> t) {
 // example1 / the headline: two spheres, a plane, the sky box (same box, ex1 1080p d5 6 spp: device-
 // resident frame 0.837 -> 0.750 ms, k_primary 1.05 -> 0.95 ms; profiles/r05_collider_seq_ab.txt)
 constexpr uint32_t MATS_SEQ_SSPC = MATS_GLOSSY_SKY | seq_bits({SRT_SPHERE, SRT_SPHERE, SRT_PLANE, SRT_CUBOID});
+// the branching scenes of two other BASELINE configs, whose frames run k_frame: example3 (floor, glass
+// cuboid, sky box; same box, ex3 1080p d8 frame 2.81 -> 2.73 ms, k_frame 2.94 -> 2.82 ms) and example4
+// (thin-film sphere, sky box; 4K frame 14.08 -> 13.96 ms), profiles/r06_collider_seq_frame_ab.txt.  The
+// cornell box's eight colliders in sequence were 1.7 % slower (4024 -> 4092 ms), so it keeps the loop.
+constexpr uint32_t MATS_SEQ_PCC = MATS_DIELECTRIC | seq_bits({SRT_PLANE, SRT_CUBOID, SRT_CUBOID});
+constexpr uint32_t MATS_SEQ_SC = MATS_FILM | seq_bits({SRT_SPHERE, SRT_CUBOID});
+#define RT_SEQ_FRAME_VARIANT(M) {M, k_primary<M, OCC>, k_trace<M, OCC>, k_frame<M, OCC>, k_trace<M, OCC, true>}
 const Variant SEQ_VARIANTS[] = {
     {MATS_SEQ_SSPC, k_primary<MATS_SEQ_SSPC, OCC>, k_trace<MATS_SEQ_SSPC, OCC>, k_frame<MATS_SEQ_SSPC, OCC>,
      k_trace<MATS_SEQ_SSPC, OCC, true>, k_primary<MATS_SEQ_SSPC, RT_FUSE_OCC, true>, k_primary_lean<MATS_SEQ_SSPC, RT_FUSE_OCC>,
      k_primary_lean<MATS_SEQ_SSPC, RT_FUSE_OCC, true>},
+#ifndef RT_EXP_MIN
+    RT_SEQ_FRAME_VARIANT(MATS_SEQ_PCC),
+    RT_SEQ_FRAME_VARIANT(MATS_SEQ_SC),
+#endif
 };
 #endif
 const Variant& pick_variant(uint32_t mats, uint32_t seq = 0) {
