@@ -342,6 +342,27 @@ int srt_intersect_collider(srt_ctx* ctx, const srt_collider* collider, const dou
  * outside the scene fails with SRT_ERR_INDEX. */
 int srt_shade(srt_ctx* ctx, const srt_trace_args* args, const int32_t* collider, const double* t,
               const double* orient, srt_stats* stats);
+/* One level of Material.get_color (materials/material.py:42-44, as get_raycolor calls it,
+ * ray.py:131-146) for a recursion the host drives through user Collider / Material subclasses
+ * (sightpy/_hybrid.py): ray i is shaded at the caller's hit as srt_shade shades it, its own colour
+ * (the terms the material adds before its children's) written to args->out_rgb, and the rays it
+ * spawns handed back instead of traced.  Child k: origin / dir, the factor its colour is multiplied
+ * by (weight; glossy.py:110, refractive.py:105-123, diffuse.py:85-124), the index of the ray it came
+ * from (parent), its medium row, depth and diffuse-reflection count.  More children than `cap`:
+ * SRT_ERR_MEMORY with `n` set to the count (call again with room for them). */
+typedef struct srt_children {
+    int64_t cap;                  /* in: room, in rays */
+    int64_t n;                    /* out: children */
+    double* origin;               /* [3][cap] */
+    double* dir;                  /* [3][cap] */
+    double* weight;               /* [3][cap] */
+    int32_t* parent;              /* [cap] */
+    int32_t* medium;              /* [cap] rows of the scene's media table */
+    int32_t* depth;               /* [cap] */
+    int32_t* diffuse_reflections; /* [cap] */
+} srt_children;
+int srt_shade_level(srt_ctx* ctx, const srt_trace_args* args, const int32_t* collider, const double* t,
+                    const double* orient, srt_children* children, srt_stats* stats);
 /* Collider.get_Normal (N [3][n]) and get_uv (uv [2][n], u then v) at points P [3][n] on the
  * collider; primitive_uv = 1 applies a Cuboid/SkyBox primitive's (4, 3) cross divide
  * (SRT_CF_UV_CROSS, cuboid.py:29-34), 0 returns the collider's own coordinates.  Either output may

@@ -1353,6 +1353,27 @@ __global__ __launch_bounds__(BLOCK) void k_seed_queue(Queue q, int64_t seg, cons
     }
 }
 
+// srt_shade_level: the children one shading level appended to the queue shards, packed in shard
+// order (block b = shard b, its rays at prefix[b] ..) into planar arrays of `total` rays
+__global__ __launch_bounds__(BLOCK) void k_gather_children(Queue q, int64_t seg, const uint32_t* cnt,
+                                                          const int64_t* prefix, int64_t total, double* O, double* D,
+                                                          double* Wt, int32_t* parent, int32_t* medium, int32_t* depth,
+                                                          int32_t* dfl) {
+    const int s = blockIdx.x;
+    const int64_t n = min((int64_t)cnt[s], seg);
+    for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
+        const Ray r = queue_load(q, (int64_t)s * seg + i);
+        const int64_t k = prefix[s] + i;
+        O[k] = r.o.x; O[total + k] = r.o.y; O[2 * total + k] = r.o.z;
+        D[k] = r.d.x; D[total + k] = r.d.y; D[2 * total + k] = r.d.z;
+        Wt[k] = r.w.x; Wt[total + k] = r.w.y; Wt[2 * total + k] = r.w.z;
+        parent[k] = (int32_t)r.pix;
+        medium[k] = (int32_t)meta_medium(r.meta);
+        depth[k] = (int32_t)meta_depth(r.meta);
+        dfl[k] = (int32_t)meta_diffuse(r.meta);
+    }
+}
+
 
 }  // namespace
 
@@ -3402,8 +3423,9 @@ int srt_stream(srt_ctx* c, void** stream) {
 
 namespace {
 // get_raycolor (srt_trace) or Material.get_color at given hits (srt_shade: fid/ft/fo non-null)
+// kids (srt_shade_level): shade the first depth only and hand its children back instead of tracing them
 int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const double* ft, const double* fo,
-               srt_stats* st) {
+               srt_stats* st, srt_children* kids = nullptr) {
     auto t_start = std::chrono::steady_clock::now();
     if (!c || !a || !a->origin || !a->dir || !a->out_rgb) return fail(SRT_ERR_ARG, "null argument");
     c->pf.valid = false;  // (slot 0's buffers are reused here)
@@ -3441,7 +3463,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
     if ((rc = ensure_queues(c, n * c->fanout))) return rc;
     // depths a->depth .. a->depth + cap (the batch's depth is a scalar in the reference)
     const int d0 = a->depth;
-    const int dlast = std::min(SRT_MAX_DEPTHS - 2, d0 + depth_cap(c));
+    const int dlast = kids ? d0 : std::min(SRT_MAX_DEPTHS - 2, d0 + depth_cap(c));
     srt_stats S{};
     std::vector<uint32_t> counts(SRT_MAX_DEPTHS * NSHARD);
     bool fx = c->deterministic;  // fixed-point colour sums (fb_add)
@@ -3496,7 +3518,7 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
             if ((flags[1] & RETRY_OVERFLOW) && (rc = ensure_queues(c, 2 * c->f->seg * NSHARD))) break;
             continue;
         }
-        if (depth_total(counts.data() + (int64_t)(dlast + 1) * NSHARD, c->f->seg) != 0) {
+        if (!kids && depth_total(counts.data() + (int64_t)(dlast + 1) * NSHARD, c->f->seg) != 0) {
             rc = fail(SRT_ERR_DEPTH, "rays alive after the depth cap");
             break;
         }
@@ -3518,6 +3540,53 @@ int trace_impl(srt_ctx* c, const srt_trace_args* a, const int32_t* fid, const do
         }
         HIP_TRY(hipMemcpyAsync(a->out_rgb, c->f->fb, (size_t)3 * n * 8, hipMemcpyDefault, c->f->stream));
         HIP_TRY(hipStreamSynchronize(c->f->stream));
+        if (kids) {
+            // the first depth's children, packed shard by shard (the order the queue appends gave them)
+            const uint32_t* kc = counts.data() + (int64_t)(d0 + 1) * NSHARD;
+            std::vector<int64_t> prefix(NSHARD);
+            int64_t total = 0;
+            for (int s = 0; s < NSHARD; ++s) {
+                prefix[s] = total;
+                total += std::min<int64_t>(kc[s], c->f->seg);
+            }
+            kids->n = total;
+            if (total > kids->cap) {
+                rc = fail(SRT_ERR_MEMORY, "children exceed srt_children.cap (n holds the count)");
+                break;
+            }
+            if (total > 0) {
+                double *kO, *kD, *kW;
+                int32_t *kp, *km, *kd, *kf;
+                int64_t* kpre;
+                HIP_TRY(bufs.alloc(&kO, 3 * total));
+                HIP_TRY(bufs.alloc(&kD, 3 * total));
+                HIP_TRY(bufs.alloc(&kW, 3 * total));
+                HIP_TRY(bufs.alloc(&kp, total));
+                HIP_TRY(bufs.alloc(&km, total));
+                HIP_TRY(bufs.alloc(&kd, total));
+                HIP_TRY(bufs.alloc(&kf, total));
+                HIP_TRY(bufs.alloc(&kpre, NSHARD));
+                HIP_TRY(hipMemcpyAsync(kpre, prefix.data(), NSHARD * 8, hipMemcpyHostToDevice, c->f->stream));
+                hipLaunchKernelGGL(k_gather_children, dim3(NSHARD), dim3(BLOCK), 0, c->f->stream, c->f->q[(d0 + 1) & 1],
+                                   c->f->seg, c->f->counts + (int64_t)(d0 + 1) * NSHARD, kpre, total, kO, kD, kW, kp, km,
+                                   kd, kf);
+                HIP_TRY(hipGetLastError());
+                for (int k = 0; k < 3; ++k) {
+                    HIP_TRY(hipMemcpyAsync(kids->origin + k * kids->cap, kO + k * total, (size_t)total * 8,
+                                           hipMemcpyDefault, c->f->stream));
+                    HIP_TRY(hipMemcpyAsync(kids->dir + k * kids->cap, kD + k * total, (size_t)total * 8,
+                                           hipMemcpyDefault, c->f->stream));
+                    HIP_TRY(hipMemcpyAsync(kids->weight + k * kids->cap, kW + k * total, (size_t)total * 8,
+                                           hipMemcpyDefault, c->f->stream));
+                }
+                HIP_TRY(hipMemcpyAsync(kids->parent, kp, (size_t)total * 4, hipMemcpyDefault, c->f->stream));
+                HIP_TRY(hipMemcpyAsync(kids->medium, km, (size_t)total * 4, hipMemcpyDefault, c->f->stream));
+                HIP_TRY(hipMemcpyAsync(kids->depth, kd, (size_t)total * 4, hipMemcpyDefault, c->f->stream));
+                HIP_TRY(hipMemcpyAsync(kids->diffuse_reflections, kf, (size_t)total * 4, hipMemcpyDefault,
+                                       c->f->stream));
+                HIP_TRY(hipStreamSynchronize(c->f->stream));
+            }
+        }
         break;
     }
     if (rc) return rc;
@@ -3537,6 +3606,16 @@ int srt_shade(srt_ctx* c, const srt_trace_args* a, const int32_t* collider, cons
               srt_stats* st) {
     if (!collider || !t || !orient) return fail(SRT_ERR_ARG, "null hit arrays");
     return trace_impl(c, a, collider, t, orient, st);
+}
+
+int srt_shade_level(srt_ctx* c, const srt_trace_args* a, const int32_t* collider, const double* t, const double* orient,
+                    srt_children* kids, srt_stats* st) {
+    if (!collider || !t || !orient || !kids) return fail(SRT_ERR_ARG, "null hit / children arrays");
+    kids->n = 0;
+    if (kids->cap < 0 || (kids->cap > 0 && (!kids->origin || !kids->dir || !kids->weight || !kids->parent ||
+                                            !kids->medium || !kids->depth || !kids->diffuse_reflections)))
+        return fail(SRT_ERR_ARG, "srt_children arrays");
+    return trace_impl(c, a, collider, t, orient, st, kids);
 }
 
 int srt_nearest(srt_ctx* c, const double* O, const double* D, int64_t n, double* t, int32_t* id, double* orient) {

@@ -66,6 +66,7 @@ class Lowered:
         self.media_keys = []
         self.scene_n = None
         self.texel_key = 0
+        self.device_index = []  # scene.collider_list index -> device collider index (-1: a user class, _hybrid)
 
     def desc(self):
         d = N.SceneDesc()
@@ -336,8 +337,17 @@ def camera_desc(cam):
 
 
 def lower_scene(scene, extra_media=()):
+    from ._hybrid import is_hybrid, device_collider, device_material
+
     L = Lowered()
     pool = _TexturePool()
+    # a scene with user Collider / Material subclasses (_hybrid.py) keeps the colliders whose geometry
+    # the device code implements (a user material's collider too: it casts shadows on the device's
+    # glossy hits, and the host never has the device shade it: its material is a black placeholder)
+    hybrid = is_hybrid(scene)
+    colliders = [c for c in scene.collider_list if device_collider(c)] if hybrid else scene.collider_list
+    dev = {id(c): i for i, c in enumerate(colliders)}
+    L.device_index = [dev.get(id(c), -1) for c in scene.collider_list]
     # ---- media: row 0 = scene.n, then each refractive material's n, then caller extras -------
     media = [_c(scene.n)]
     keys = [tuple(media[0])]
@@ -354,7 +364,7 @@ def lower_scene(scene, extra_media=()):
 
     materials, mat_index = [], {}
     prims = []
-    for c in scene.collider_list:
+    for c in colliders:
         m = c.assigned_primitive.material
         if id(m) not in mat_index:
             mat_index[id(m)] = len(materials)
@@ -374,6 +384,11 @@ def lower_scene(scene, extra_media=()):
     for i, m in enumerate(materials):
         r = mrecs[i]
         p = np.zeros(N.SRT_MATERIAL_PARAMS)
+        if hybrid and not device_material(m):
+            r["type"] = N.EMISSIVE  # (placeholder: never shaded on the device)
+            r["p"] = p
+            mrecs[i] = r
+            continue
         if getattr(m, "normalmap_u8", None) is not None:
             r["normalmap"] = pool.add(m.normalmap_u8, _RAW_LUT, repeat=m.repeat)
         if isinstance(m, Glossy):
@@ -443,9 +458,9 @@ def lower_scene(scene, extra_media=()):
 
     # ---- colliders --------------------------------------------------------------------------
     shadow_ids = {id(c) for c in scene.shadowed_collider_list}
-    crecs = np.zeros(len(scene.collider_list), dtype=N.COLLIDER_DTYPE)
+    crecs = np.zeros(len(colliders), dtype=N.COLLIDER_DTYPE)
     prim_index = {}
-    for i, c in enumerate(scene.collider_list):
+    for i, c in enumerate(colliders):
         prim = c.assigned_primitive
         rec = collider_record(c)
         rec["material"] = mat_index[id(prim.material)]
@@ -470,16 +485,16 @@ def lower_scene(scene, extra_media=()):
             raise AttributeError("'Sphere_Collider' object has no attribute 'inverse_basis_matrix'")
         crecs[i] = rec
     L.colliders = crecs
-    L.max_ray_depth = int(max([int(c.assigned_primitive.max_ray_depth) for c in scene.collider_list], default=0))
+    L.max_ray_depth = int(max([int(c.assigned_primitive.max_ray_depth) for c in colliders], default=0))
 
     # ---- lights -----------------------------------------------------------------------------
     lrecs = np.zeros(len(scene.Light_list), dtype=N.LIGHT_DTYPE)
-    light_local = np.zeros((len(scene.Light_list), len(scene.collider_list), 3))
+    light_local = np.zeros((len(scene.Light_list), len(colliders), 3))
     for i, lt in enumerate(scene.Light_list):
         if isinstance(lt, DirectionalLight):
             lrecs[i]["type"] = N.LIGHT_DIRECTIONAL
             lrecs[i]["dir"] = _f3(lt.Ldir)
-            for j, c in enumerate(scene.collider_list):
+            for j, c in enumerate(colliders):
                 if isinstance(c, Cuboid_Collider):
                     # shadow rays: D is a scalar vec3, so D.matmul goes through BLAS gemv
                     light_local[i, j] = _f3(lt.Ldir.matmul(c.basis_matrix))

@@ -208,6 +208,21 @@ class TraceArgs(ctypes.Structure):
     ]
 
 
+class Children(ctypes.Structure):
+    """srt_children: the rays one level of shading spawns (srt_shade_level)."""
+    _fields_ = [
+        ("cap", ctypes.c_int64),
+        ("n", ctypes.c_int64),
+        ("origin", _p),
+        ("dir", _p),
+        ("weight", _p),
+        ("parent", _p),
+        ("medium", _p),
+        ("depth", _p),
+        ("diffuse_reflections", _p),
+    ]
+
+
 # name -> (restype, argtypes) for every entry point of include/sightpy_rt.h
 RENDER_ASYNC, RENDER_SHARDED, RENDER_GATHER_RGB, RENDER_RGB_ROWS, RENDER_RGB_LOCAL, RENDER_RGBX = 1, 2, 4, 8, 16, 32  # SRT_RENDER_*
 ABI_VERSION = 5  # SRT_ABI_VERSION of include/sightpy_rt.h
@@ -225,6 +240,8 @@ SIGNATURES = {
     "srt_nearest": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, _p, _p]),
     "srt_intersect_collider": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_int64, _p]),
     "srt_shade": (ctypes.c_int, [_p, ctypes.POINTER(TraceArgs), _p, _p, _p, ctypes.POINTER(Stats)]),
+    "srt_shade_level": (ctypes.c_int, [_p, ctypes.POINTER(TraceArgs), _p, _p, _p, ctypes.POINTER(Children),
+                                       ctypes.POINTER(Stats)]),
     "srt_collider_surface": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, _p, ctypes.c_int]),
     "srt_texture_lookup": (ctypes.c_int, [_p, _p, _p, ctypes.c_int64, _p, ctypes.c_int64, _p]),
     "srt_primary_rays": (ctypes.c_int, [_p, ctypes.POINTER(CameraDesc), _p, _p, _p]),

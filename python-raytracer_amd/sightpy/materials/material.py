@@ -3,7 +3,9 @@
 A material here is a parameter record.  Its `get_color(scene, ray, hit)` — the reference's
 per-batch shading entry point — runs on the device (`srt_shade`): the shading kernels in
 `csrc/rt_device.h` (`rt_shade_*`) implement each subclass, and the reflected / refracted /
-diffuse rays a hit spawns are traced to completion as in get_raycolor.  Normal maps
+diffuse rays a hit spawns are traced to completion as in get_raycolor.  In a scene holding user
+Collider / Material subclasses the children are traced by the host-driven recursion instead
+(`sightpy/_hybrid.py`: one device shading level per call).  Normal maps
 (material.py:18-40) are supported for Plane and Cuboid colliders (the only ones with
 `inverse_basis_matrix`), in shading and through get_Normal (srt_material_normal).
 """
@@ -43,9 +45,12 @@ class Material:
         """Colour of the batch `ray` at `hit` (all rays hit `hit.collider` at `hit.distance` with
         `hit.orientation`), as get_raycolor adds it (ray.py:131-146): srt_shade on the device."""
         from .._backend import trace_rays
+        from .. import _hybrid
 
         if hit.collider.assigned_primitive.material is not self:
             raise ValueError("a hit is shaded by the material of its collider's primitive")
-        ids = scene.collider_list.index(hit.collider)
         hit.point = ray.origin + ray.dir * hit.distance
+        if _hybrid.is_hybrid(scene):  # user classes in the scene: one level here, the children traced by _hybrid
+            return _hybrid.shade_level(scene, self, ray, hit)
+        ids = scene.collider_list.index(hit.collider)
         return trace_rays(ray, scene, hits=(ids, hit.distance, hit.orientation))

@@ -3,7 +3,9 @@
 `Ray` and `Hit` keep the reference's batch containers.  `get_raycolor(ray, scene)` — the
 reference's recursive numpy driver (ray.py:122-148) — is served by the device wavefront tracer:
 the batch is uploaded, traced to completion by the HIP kernels (intersect -> nearest -> shade ->
-child rays, depth by depth) and the per-ray colours are returned.  `get_distances` is the
+child rays, depth by depth) and the per-ray colours are returned.  A scene holding user subclasses of
+Collider / Material (duck-typed plugins) goes through `_hybrid.raycolor`, this recursion driven
+from the host with the device doing every built-in step.  `get_distances` is the
 nearest-hit probe (ray.py:151-163).
 """
 import numpy as np
@@ -87,16 +89,24 @@ class Hit:
 
 
 def get_raycolor(ray, scene):
-    """Colour of every ray of the batch (reference ray.py:122-148), traced on the GPU."""
+    """Colour of every ray of the batch (reference ray.py:122-148), traced on the GPU; a scene with
+    user Collider / Material subclasses through the host-driven recursion (_hybrid.py)."""
     from ._backend import trace_rays
+    from . import _hybrid
 
+    if _hybrid.is_hybrid(scene):
+        return _hybrid.raycolor(ray, scene)
     return trace_rays(ray, scene)
 
 
 def get_distances(ray, scene):
     """Grey map min(nearest, 10)/10 of the batch (reference ray.py:151-163), on the GPU."""
     from ._backend import nearest_hits
+    from . import _hybrid
 
-    t, _, _ = nearest_hits(scene, ray.origin, ray.dir)
+    if _hybrid.is_hybrid(scene):
+        t = _hybrid.nearest_distance(ray, scene)
+    else:
+        t, _, _ = nearest_hits(scene, ray.origin, ray.dir)
     g = np.where(t <= 10, t, 10) / 10
     return rgb(g, g, g)

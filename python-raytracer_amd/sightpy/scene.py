@@ -76,12 +76,23 @@ class Scene:
         on the number of GPUs.
         """
         from . import _backend as B
+        from . import _hybrid
 
         print("Rendering...")
         t0 = time.time()
         if rng not in ("numpy", "numpy-host", "device"):
             raise ValueError("rng must be 'numpy', 'numpy-host' or 'device'")
         H, W = int(self.camera.screen_height), int(self.camera.screen_width)
+        if _hybrid.is_hybrid(self):
+            # user Collider / Material subclasses: the reference's recursion driven from the host,
+            # the built-in steps on the device (_hybrid.py); numpy's stream as the reference draws it
+            from .utils.colour_functions import sRGB_linear_to_sRGB
+
+            lin = _hybrid.render_linear(self, samples_per_pixel)
+            color = sRGB_linear_to_sRGB(lin.to_array())
+            u8 = [(255 * np.clip(c, 0, 1).reshape((H, W))).astype(np.uint8) for c in color]
+            print("Render Took", time.time() - t0)
+            return Image.fromarray(np.stack(u8, axis=-1), "RGB")
         ndev = len(B.devices())
         if ndev > 1 and rng != "numpy-host" and H >= 8 * ndev:
             out = B.render_group(self, samples_per_pixel, seed=seed, batch_size=batch_size, want_rgb=False,
@@ -110,9 +121,16 @@ class Scene:
 
         print("Rendering...")
         t0 = time.time()
+        from . import _hybrid
+
         jitter = self.camera.draw_jitter(1)[0]
         O, D = primary_rays(self.camera, jitter)
-        t, _, _ = nearest_hits(self, O, D)
+        if _hybrid.is_hybrid(self):
+            from .ray import Ray
+
+            t = _hybrid.nearest_distance(Ray(vec3(*O), vec3(*D), 0, self.n, 0, 0, 0), self)
+        else:
+            t, _, _ = nearest_hits(self, O, D)
         g = np.where(t <= 10, t, 10) / 10
         print("Render Took", time.time() - t0)
         h, w = self.camera.screen_height, self.camera.screen_width

@@ -73,7 +73,8 @@ PROBE = r"""
 #define O(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
   S(srt_collider) S(srt_material) S(srt_texture) S(srt_light) S(srt_scene_desc) S(srt_camera)
-  S(srt_render_args) S(srt_stats) S(srt_trace_args) S(srt_mt_state)
+  S(srt_render_args) S(srt_stats) S(srt_trace_args) S(srt_mt_state) S(srt_children)
+  O(srt_children, diffuse_reflections)
   O(srt_collider, p) O(srt_material, p) O(srt_texture, lut) O(srt_stats, total_rays)
   O(srt_render_args, out_hit_id) O(srt_render_args, seed) O(srt_camera, xs)
   return 0;
@@ -99,8 +100,10 @@ def test_struct_layout_matches_binding(tmp_path):
     assert vals["srt_material.p"] == N.MATERIAL_DTYPE.fields["p"][1]
     assert vals["srt_texture.lut"] == N.TEXTURE_DTYPE.fields["lut"][1]
     for name, cls in (("srt_scene_desc", N.SceneDesc), ("srt_camera", N.CameraDesc),
-                      ("srt_render_args", N.RenderArgs), ("srt_stats", N.Stats), ("srt_trace_args", N.TraceArgs)):
+                      ("srt_render_args", N.RenderArgs), ("srt_stats", N.Stats), ("srt_trace_args", N.TraceArgs),
+                      ("srt_children", N.Children)):
         assert vals[name] == ctypes.sizeof(cls), name
+    assert vals["srt_children.diffuse_reflections"] == N.Children.diffuse_reflections.offset
     assert vals["srt_stats.total_rays"] == N.Stats.total_rays.offset
     assert vals["srt_render_args.out_hit_id"] == N.RenderArgs.out_hit_id.offset
     assert vals["srt_render_args.seed"] == N.RenderArgs.seed.offset
