@@ -641,6 +641,32 @@ __device__ __forceinline__ void store_u8_chunk(uint8_t* dst, const uint8_t px[3]
     }
 }
 
+// The uint8 RGB of a tw x th pixel tile (lane l < tw th holds local pixel (row0 + l / tw, col0 + l % tw))
+// of a frame of W columns and nrows rows: per tile row of tw = 8 (4) pixels, 6 (3) dword stores when
+// the row is whole and dword-aligned, else byte stores.  Every lane of the wave must call it.
+__device__ __forceinline__ void store_u8_tile(uint8_t* out, const uint8_t px[3], int lane, int tw, int th,
+                                              int64_t row0, int64_t col0, int64_t W, int64_t nrows) {
+    const uint32_t v = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+    const int nd = (3 * tw) / 4;  // dwords per tile row
+    const int ry = lane / nd, w = lane % nd;
+    const int q0 = (4 * w) / 3, r0 = (4 * w) % 3;
+    const uint32_t x0 = __shfl(v, ry * tw + q0), x1 = __shfl(v, ry * tw + q0 + 1);
+    const int64_t row = row0 + ry;
+    uint8_t* dst = out + 3 * (row * W + col0);
+    const bool whole = col0 + tw <= W && (reinterpret_cast<uintptr_t>(dst) & 3) == 0;
+    if (ry < th && row < nrows && whole) reinterpret_cast<uint32_t*>(dst)[w] = (x0 >> (8 * r0)) | (x1 << (8 * (3 - r0)));
+    // rows that are cut by the frame's edge or unaligned: byte stores by the pixel's own lane
+    const int py = lane / tw, pxl = lane % tw;
+    const int64_t prow = row0 + py, pcol = col0 + pxl;
+    uint8_t* pd = out + 3 * (prow * W + col0);
+    const bool pwhole = col0 + tw <= W && (reinterpret_cast<uintptr_t>(pd) & 3) == 0;
+    if (lane < tw * th && prow < nrows && pcol < W && !pwhole) {
+        pd[3 * pxl] = px[0];
+        pd[3 * pxl + 1] = px[1];
+        pd[3 * pxl + 2] = px[2];
+    }
+}
+
 // Depth 0: primary-ray generation (camera.py:51-85) fused with the trace step.  A wave takes
 // ppw = 64 / G consecutive pixels of the pass: lane l traces pixel l % ppw through the samples of
 // its sample group l / ppw (G = P.pix_groups, a power of two; G > 1 gives a small frame -- one GPU's
