@@ -1836,6 +1836,8 @@ int pix_groups(const srt_ctx* c, int64_t npix, int ns, bool fused) {
     // the fused kernel 1.095 -> 1.050 ms per launch, device-resident frame 0.841 -> 0.830 ms
     // (profiles/r04_pix_groups_ab.txt)
     if (fused && g < 2 && ns % 2 == 0) g = 2;
+    // the fused paths' tiles of 8 x 64 / g pixels (rt_primary_body.inc) need g <= 8
+    if (fused && !(c->mats & MAT_BVH)) g = std::min(g, 8);
     return g;
 }
 
