@@ -813,6 +813,21 @@ __device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// k_frame's tile: 8 x 8 pixels of the pass or 64 consecutive ones of a row; the tile's first pixel is
+// tile0, and the LDS accumulator of pixel tile0 + d is the lane that owns it.  A square tile's rays
+// stay coherent deeper (fewer chunks mix colliders): same box, ex3 1080p d8 frame 2.755 -> 2.605 ms,
+// cornell 800x800 512 spp 4006 -> 3939 ms, but the thin-film example4 4K 13.95 -> 14.09 ms, so the
+// thin-film variants keep rows (profiles/r06_frame_tile_ab.txt).
+constexpr bool frame_tile_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFILM)) == 0; }
+__device__ __forceinline__ uint32_t frame_tile_index(bool tiled, uint32_t d, uint32_t W) {
+    if (!tiled) return d;
+    const uint32_t ly = d / W;
+    return ly * 8u + (d - ly * W);
+}
+inline int64_t frame_tiles(bool tiled, int64_t W, int64_t nrows) {
+    return tiled ? ((W + 7) / 8) * ((nrows + 7) / 8) : (W * nrows + FRAME_BLOCK - 1) / FRAME_BLOCK;
+}
+
 struct FrameEmit {
     const TraceParams& P;
     const Ray& r;
@@ -821,10 +836,11 @@ struct FrameEmit {
     FrameLds* L;
     uint32_t tile0;
     int64_t ring_base;
+    bool tiled;  // (k_frame's FRAME_TILE)
 
     __device__ void local(d3 c) const {
         if (is_zero(c)) return;
-        const uint32_t k = r.pix - tile0;
+        const uint32_t k = frame_tile_index(tiled, r.pix - tile0, (uint32_t)P.cam.width);
         __hip_atomic_fetch_add(&L->acc[0][k], r.w.x * c.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(&L->acc[1][k], r.w.y * c.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(&L->acc[2][k], r.w.z * c.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -883,6 +899,7 @@ struct FrameEmit {
 
 template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
+    constexpr bool FRAME_TILE = frame_tile_for(MATS);
     const TraceParams& P = P0;
     {
         const int nl = P.S.nlut_lds;
@@ -905,7 +922,9 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     __syncthreads();
     RT_ACC(18, tf0);
     const uint32_t tile = blockIdx.x % (uint32_t)P.ntiles, grp = blockIdx.x / (uint32_t)P.ntiles;
-    const uint32_t tile0 = tile * FRAME_BLOCK;
+    const uint32_t Wc = (uint32_t)P.cam.width, nrows = (uint32_t)(P.npix / P.cam.width);
+    const uint32_t tiles_x = (Wc + 7u) >> 3, ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const uint32_t tile0 = FRAME_TILE ? (ty * 8u) * Wc + tx * 8u : tile * FRAME_BLOCK;
     const int spg = (P.spp + P.groups - 1) / P.groups;
     const int s_end = min(P.spp, (int)(grp + 1) * spg);
     const int64_t ring_base = (int64_t)L.slot * P.ring_cap;
@@ -913,10 +932,20 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     uint32_t err = 0;
     uint32_t shadow = 0;
     // this lane's pixel of the tile
-    const uint32_t p = tile0 + lane;
-    const bool pact = p < (uint32_t)P.npix;
-    const uint32_t lr = pact ? p / (uint32_t)P.cam.width : 0u;
-    const uint32_t col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
+    uint32_t p, lr, col;
+    bool pact;
+    if (FRAME_TILE) {
+        const uint32_t r = ty * 8u + (lane >> 3), cx = tx * 8u + (lane & 7u);
+        pact = r < nrows && cx < Wc;
+        lr = pact ? r : 0u;
+        col = pact ? cx : 0u;
+        p = pact ? lr * Wc + col : tile0;
+    } else {
+        p = tile0 + lane;
+        pact = p < (uint32_t)P.npix;
+        lr = pact ? p / (uint32_t)P.cam.width : 0u;
+        col = pact ? p - lr * (uint32_t)P.cam.width : 0u;
+    }
     const int grow = pact ? P.rows[lr] : 0;
     const double xc = pact ? P.cam.xs[col] : 0.0, yr = pact ? P.cam.ys[grow] : 0.0;
     const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
@@ -970,7 +999,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             if ((int)depth > P.dcap) active = false;
         }
         RT_T0(tt2);
-        trace_one<MATS>(P, r, active, err, hs, FrameEmit{P, r, 0u, &shadow, &L, tile0, ring_base});
+        trace_one<MATS>(P, r, active, err, hs, FrameEmit{P, r, 0u, &shadow, &L, tile0, ring_base, FRAME_TILE});
         RT_ACC(17, tt2);
     }
     RT_T0(te0);
@@ -985,8 +1014,12 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             if (P.out_rgb) { P.out_rgb[p] = rr; P.out_rgb[P.npix + p] = gg; P.out_rgb[2 * P.npix + p] = bb; }
         }
         if (P.out_u8) {
-            const int64_t p0 = p - lane;
-            store_u8_chunk(P.out_u8 + 3 * p0, px, lane, (int)min<int64_t>(64, P.npix - p0));
+            if (FRAME_TILE) {
+                store_u8_tile(P.out_u8, px, lane, 8, 8, (int64_t)(ty * 8u), (int64_t)(tx * 8u), (int64_t)Wc, (int64_t)nrows);
+            } else {
+                const int64_t p0 = p - lane;
+                store_u8_chunk(P.out_u8 + 3 * p0, px, lane, (int)min<int64_t>(64, P.npix - p0));
+            }
         }
     } else if (pact && P.groups > 1) {
         double* part = P.fbg + (int64_t)grp * 3 * P.npix;
@@ -2826,7 +2859,7 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
     F.cnt_words = (int64_t)SRT_MAX_DEPTHS * NSHARD;
     F.pass_words = F.cnt_words + 2;
     F.frame = c->use_frame < 0 ? c->fanout > 1 : c->use_frame != 0;
-    const int64_t ntiles = (npix + FRAME_BLOCK - 1) / FRAME_BLOCK;
+    const int64_t ntiles = frame_tiles(frame_tile_for(pick_variant(c->mats, c->seq_on ? c->seq : 0).mats), W, npix / W);
     if (F.frame) {
         // a frame kernel block traces one 64-pixel tile through the pass's samples: a small frame (a
         // shard of a multi-GPU frame) has too few tiles to fill the GPU, so its samples are split
