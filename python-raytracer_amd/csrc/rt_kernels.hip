@@ -819,6 +819,11 @@ __device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
 // cornell 800x800 512 spp 4006 -> 3939 ms, but the thin-film example4 4K 13.95 -> 14.09 ms, so the
 // thin-film variants keep rows (profiles/r06_frame_tile_ab.txt).
 constexpr bool frame_tile_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFILM)) == 0; }
+// k_frame's ring drained newest first (a stack: the chunk taken is the last 64 rays pushed, usually
+// the children of the chunk just traced, still in L2) for the thin-film variants: ex4 4K frame 13.83 ->
+// 13.58 ms; oldest first for the rest (ex3 unchanged, cornell's Diffuse fan-out outgrows a stack's
+// ring: 4.02 -> 5.24 s; profiles/r06_rejected_frame_lifo.txt)
+constexpr bool frame_lifo_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFILM)) != 0; }
 __device__ __forceinline__ uint32_t frame_tile_index(bool tiled, uint32_t d, uint32_t W) {
     if (!tiled) return d;
     const uint32_t ly = d / W;
@@ -899,7 +904,7 @@ struct FrameEmit {
 
 template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
-    constexpr bool FRAME_TILE = frame_tile_for(MATS);
+    constexpr bool FRAME_TILE = frame_tile_for(MATS), FRAME_LIFO = frame_lifo_for(MATS);
     const TraceParams& P = P0;
     {
         const int nl = P.S.nlut_lds;
@@ -960,18 +965,25 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
         uint32_t depth = 0;
         int32_t* hs = nullptr;
         if (pending >= (uint32_t)FRAME_BLOCK || s_next >= s_end) {
-            // a chunk of the ring
+            // a chunk of the ring: its oldest rays, or (FRAME_LIFO) its newest, whose children are then
+            // pushed over them (their stores follow every lane's loads: the loaded rays are read first)
             const uint32_t take = min(pending, (uint32_t)FRAME_BLOCK);
             active = lane < take;
             RT_T0(tl0);
+            const uint32_t first = FRAME_LIFO ? tail - take : head;
             if (active) {
-                r = queue_load(P.ring, ring_base + (int64_t)((head + lane) & (uint32_t)(P.ring_cap - 1)));
+                r = queue_load(P.ring, ring_base + (int64_t)((first + lane) & (uint32_t)(P.ring_cap - 1)));
                 depth = meta_depth(r.meta);
             } else {
                 r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
                 r.pix = tile0; r.meta = 0; r.path = 0;
             }
-            if (lane == 0) lds_put(&L.head, head + take);
+            if (lane == 0) {
+                if (FRAME_LIFO)
+                    lds_put(&L.tail, first);
+                else
+                    lds_put(&L.head, head + take);
+            }
             RT_ACC(16, tl0);
         } else {
             // primary rays of sample s_next for the tile's pixels (camera.py:51-85)
