@@ -69,3 +69,27 @@ def test_gpu_user_classes_get_distances():
     want = np.minimum.reduce(dists)
     assert np.array_equal(near, want)
     assert np.array_equal(np.asarray(g.x), np.where(want <= 10, want, 10) / 10)
+
+
+def test_gpu_user_floor_under_builtin_glass():
+    """A built-in Refractive cuboid (srt_shade_level returns its reflected and refracted children,
+    the refracted ones in the glass's medium) over a user-material floor: the frame equals the
+    reference recursion on the CPU."""
+    from sightpy import _hybrid
+    from sightpy.ray import get_raycolor
+
+    W, H, spp = 40, 30, 2
+    sc = U.glass_scene(W, H, 4)
+    np.random.seed(17)
+    state = np.random.get_state()
+    jit = sc.camera.draw_jitter(spp)
+    U.TRACE["fn"] = hybrid_ref.trace
+    ref = hybrid_ref.render_linear(sc, jit)
+    U.TRACE["fn"] = get_raycolor
+    np.random.set_state(state)
+    lin = _hybrid.render_linear(sc, spp)
+    got = np.array([np.broadcast_to(np.asarray(c, dtype=np.float64), (W * H,)) for c in (lin.x, lin.y, lin.z)])
+    nz = ref != 0.0
+    assert np.all(got[~nz] == 0.0)
+    rel = np.abs(got[nz] - ref[nz]) / np.abs(ref[nz])
+    assert rel.max() <= 1e-5, rel.max()

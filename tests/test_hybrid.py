@@ -79,3 +79,4 @@ def test_expected_frame_harness_equals_the_oracle_without_user_classes():
     ref, _, _ = O.render_linear(sc, jit)
     got = hybrid_ref.render_linear(sc, jit)
     assert np.array_equal(got, ref)
+

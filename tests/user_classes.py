@@ -95,3 +95,24 @@ def scene(kind, width=48, height=36, depth=3):
                  u_axis=vec3(1.0, 0, 0), v_axis=vec3(0, 0, -1.0), max_ray_depth=depth))
     sc.add_Background("stormydays.png")
     return sc
+
+
+def glass_scene(width=40, height=30, depth=4):
+    """example3's glass cuboid (built-in Refractive: two children per hit, rays inside the glass in
+    its medium) over a floor whose material is a user Tinted: srt_shade_level's children carry media
+    rows back to the host recursion."""
+    from sightpy import Scene, Plane, Cuboid, Refractive
+
+    green = Refractive(n=vec3(1.5 + 4e-8j, 1.5 + 0.0j, 1.5 + 4e-8j))
+    sc = Scene()
+    sc.add_Camera(look_from=vec3(0.0, 0.25, 1.0), look_at=vec3(0.0, 0.25, -3.0), screen_width=width,
+                  screen_height=height)
+    sc.add_DirectionalLight(Ldir=vec3(0.0, 0.5, 0.5), color=rgb(0.5, 0.5, 0.5))
+    sc.add(Plane(material=Tinted(rgb(0.7, 0.6, 0.4), 0.3), center=vec3(0, -0.5, -3.0), width=6.0, height=6.0,
+                 u_axis=vec3(1.0, 0, 0), v_axis=vec3(0, 0, -1.0), max_ray_depth=depth))
+    cb = Cuboid(material=green, center=vec3(0.00, 0.0001, -0.8), width=0.9, height=1.0, length=0.4, shadow=False,
+                max_ray_depth=depth)
+    cb.rotate(θ=30, u=vec3(0, 1, 0))
+    sc.add(cb)
+    sc.add_Background("stormydays.png")
+    return sc
