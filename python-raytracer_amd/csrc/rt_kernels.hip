@@ -798,6 +798,7 @@ struct FrameLds {
     uint32_t depth_cnt[SRT_MAX_DEPTHS];
     uint32_t head, tail;         // ring positions (wave-uniform; kept in LDS so that updates made
                                  // under divergent control flow are seen by every lane)
+    uint32_t head1, tail1;       // (FRAME_SPLIT) the second ring's: rays travelling inside a medium
     uint32_t slot;
     uint32_t overflow;
 };
@@ -824,6 +825,14 @@ constexpr bool frame_tile_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFI
 // 13.58 ms; oldest first for the rest (ex3 unchanged, cornell's Diffuse fan-out outgrows a stack's
 // ring: 4.02 -> 5.24 s; profiles/r06_rejected_frame_lifo.txt)
 constexpr bool frame_lifo_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFILM)) != 0; }
+// k_frame's ring split in two halves for the refractive variants without thin films or Diffuse: rays
+// travelling inside a medium (which next hit the body they are in) in one, the rest in the other, so
+// that a chunk of the first shades one collider in one pass of the material waterfall: ex3 1080p d8
+// frame 2.647 -> 2.552 ms, k_frame 2.86 -> 2.65 ms; the thin-film example4 4K 13.53 -> 14.04 ms, and
+// cornell's Diffuse fan-out overflows half a ring (profiles/r06_frame_split_ab.txt)
+constexpr bool frame_split_for(uint32_t mats) {
+    return (mats & mat_bit(SRT_REFRACTIVE)) != 0 && (mats & (mat_bit(SRT_THINFILM) | mat_bit(SRT_DIFFUSE))) == 0;
+}
 __device__ __forceinline__ uint32_t frame_tile_index(bool tiled, uint32_t d, uint32_t W) {
     if (!tiled) return d;
     const uint32_t ly = d / W;
@@ -842,6 +851,7 @@ struct FrameEmit {
     uint32_t tile0;
     int64_t ring_base;
     bool tiled;  // (k_frame's FRAME_TILE)
+    bool split;  // (k_frame's FRAME_SPLIT) rays inside a medium (child medium != 0) go to ring 1
 
     __device__ void local(d3 c) const {
         if (is_zero(c)) return;
@@ -867,17 +877,37 @@ struct FrameEmit {
         base = (uint32_t)__shfl((int)base, leader);
         return base + below;
     }
-    __device__ void store(uint32_t pos, const Child& c, uint32_t path) const {
+    // ring q (split: half the slot each) at its position pos
+    __device__ void store(uint32_t pos, const Child& c, uint32_t path, int q = 0) const {
         const uint32_t depth = meta_depth(r.meta) + 1;
-        if (pos - lds_get(&L->head) >= (uint32_t)P.ring_cap) {  // ring full: the frame is re-rendered with bigger rings
+        const uint32_t cap = split ? (uint32_t)P.ring_cap >> 1 : (uint32_t)P.ring_cap;
+        if (pos - lds_get(q ? &L->head1 : &L->head) >= cap) {  // ring full: the frame is re-rendered with bigger rings
             lds_put(&L->overflow, 1u);
             return;
         }
-        queue_store(P.ring, ring_base + (int64_t)(pos & (uint32_t)(P.ring_cap - 1)), c.o, c.d, mul(r.w, c.w), r.pix,
-                    pack_meta(c.medium, depth, c.dfl), path);
+        queue_store(P.ring, ring_base + (int64_t)(q ? cap : 0u) + (int64_t)(pos & (cap - 1u)), c.o, c.d, mul(r.w, c.w),
+                    r.pix, pack_meta(c.medium, depth, c.dfl), path);
     }
     __device__ void child(const Child& c) const {
-        store(reserve(1u), c, child_path(r.path, c.slot, round));
+        if (!split) {
+            store(reserve(1u), c, child_path(r.path, c.slot, round));
+            return;
+        }
+        // a ray inside a medium (a refractive body: it next hits that body from inside) to ring 1, the
+        // rest to ring 0, so that chunks of ring 1 shade one collider in one waterfall pass
+        const bool in = c.medium != 0u;
+        const uint64_t m1 = __ballot(in), m0 = __ballot(!in), act = __ballot(1);
+        const int leader = __builtin_ctzll(act);
+        uint32_t b0 = 0, b1 = 0;
+        if (lanes_below(act) == 0) {
+            if (m0) b0 = __hip_atomic_fetch_add(&L->tail, (uint32_t)__builtin_popcountll(m0), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (m1) b1 = __hip_atomic_fetch_add(&L->tail1, (uint32_t)__builtin_popcountll(m1), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        b0 = (uint32_t)__shfl((int)b0, leader);
+        b1 = (uint32_t)__shfl((int)b1, leader);
+        store(in ? b1 + lanes_below(m1) : b0 + lanes_below(m0), c, child_path(r.path, c.slot, round), in ? 1 : 0);
     }
     // the fan-out child-major in the ring (as GpuEmit::diffuse): the k-th children of the lanes are
     // consecutive, every store a coalesced run.  Lane-major positions scattered each store over 64
@@ -905,6 +935,7 @@ struct FrameEmit {
 template <uint32_t MATS, int OCC = 2>
 __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     constexpr bool FRAME_TILE = frame_tile_for(MATS), FRAME_LIFO = frame_lifo_for(MATS);
+    constexpr bool FRAME_SPLIT = frame_split_for(MATS);
     const TraceParams& P = P0;
     {
         const int nl = P.S.nlut_lds;
@@ -922,6 +953,8 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
         L.slot = s;
         L.head = 0u;
         L.tail = 0u;
+        L.head1 = 0u;
+        L.tail1 = 0u;
         L.overflow = 0u;
     }
     __syncthreads();
@@ -956,10 +989,20 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
     const uint32_t gpix = (uint32_t)grow * (uint32_t)P.cam.width + col;
     const Quot qw((double)P.cam.width), qh((double)P.cam.height);
     int s_next = (int)grp * spg;
+    const uint32_t rcap = FRAME_SPLIT ? (uint32_t)P.ring_cap >> 1 : (uint32_t)P.ring_cap;  // rays per ring
     for (;;) {
-        const uint32_t head = lds_get(&L.head), tail = lds_get(&L.tail);
-        const uint32_t pending = tail - head;
-        if (pending == 0u && s_next >= s_end) break;
+        const uint32_t head0 = lds_get(&L.head), tail0 = lds_get(&L.tail);
+        const uint32_t head1 = FRAME_SPLIT ? lds_get(&L.head1) : 0u, tail1 = FRAME_SPLIT ? lds_get(&L.tail1) : 0u;
+        const uint32_t pend0 = tail0 - head0, pend1 = tail1 - head1;
+        if (pend0 == 0u && pend1 == 0u && s_next >= s_end) break;
+        // a ring overflowed: the frame is re-rendered with bigger rings, and the positions past the
+        // overflow hold no rays of this launch
+        if (lds_get(&L.overflow)) break;
+        // the ring a chunk comes from: the fuller of two full chunks (ring 1 on a tie), else the one
+        // holding a full chunk, else (primaries done) ring 1 then ring 0
+        const int q = pend1 >= (uint32_t)FRAME_BLOCK ? (pend1 >= pend0 ? 1 : 0)
+                                                     : (pend0 < (uint32_t)FRAME_BLOCK && pend1 > 0u ? 1 : 0);
+        const uint32_t head = q ? head1 : head0, tail = q ? tail1 : tail0, pending = q ? pend1 : pend0;
         Ray r;
         bool active;
         uint32_t depth = 0;
@@ -972,7 +1015,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             RT_T0(tl0);
             const uint32_t first = FRAME_LIFO ? tail - take : head;
             if (active) {
-                r = queue_load(P.ring, ring_base + (int64_t)((first + lane) & (uint32_t)(P.ring_cap - 1)));
+                r = queue_load(P.ring, ring_base + (int64_t)(q ? rcap : 0u) + (int64_t)((first + lane) & (rcap - 1u)));
                 depth = meta_depth(r.meta);
             } else {
                 r.o = r.d = r.w = d3{0.0, 0.0, 0.0};
@@ -980,9 +1023,9 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             }
             if (lane == 0) {
                 if (FRAME_LIFO)
-                    lds_put(&L.tail, first);
+                    lds_put(q ? &L.tail1 : &L.tail, first);
                 else
-                    lds_put(&L.head, head + take);
+                    lds_put(q ? &L.head1 : &L.head, head + take);
             }
             RT_ACC(16, tl0);
         } else {
@@ -1011,7 +1054,7 @@ __global__ __launch_bounds__(FRAME_BLOCK, OCC) void k_frame(TraceParams P0) {
             if ((int)depth > P.dcap) active = false;
         }
         RT_T0(tt2);
-        trace_one<MATS>(P, r, active, err, hs, FrameEmit{P, r, 0u, &shadow, &L, tile0, ring_base, FRAME_TILE});
+        trace_one<MATS>(P, r, active, err, hs, FrameEmit{P, r, 0u, &shadow, &L, tile0, ring_base, FRAME_TILE, FRAME_SPLIT});
         RT_ACC(17, tt2);
     }
     RT_T0(te0);
@@ -3022,7 +3065,9 @@ int render_impl(srt_ctx* c, const srt_camera* cam, const srt_render_args* a, srt
             if (!r && gather_rgb) r = ensure_buf(&c->f->g_rgb, c->f->g_rgb_cap, c->nranks * maxpix * 3);
             if (!r && gather_rgb) r = ensure_buf(&c->f->full_rgb, c->f->full_rgb_cap, 3 * W * Hf);
         }
-        if (!r) r = F.frame ? ensure_ring(c, (int64_t)FRAME_BLOCK * (c->fanout + 2) * 2)
+        // (a split ring: each half that size)
+        if (!r) r = F.frame ? ensure_ring(c, (int64_t)FRAME_BLOCK * (c->fanout + 2) * 2 *
+                                                 (frame_split_for(pick_variant(c->mats, c->seq_on ? c->seq : 0).mats) ? 2 : 1))
                             : ensure_queues(c, (int64_t)batch * npix * c->fanout);
         if (!r && (int)c->f->ev.size() < F.npass * F.nev) {
             for (hipEvent_t e : c->f->ev) (void)hipEventDestroy(e);
