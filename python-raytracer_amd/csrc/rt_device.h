@@ -87,6 +87,8 @@ constexpr uint32_t MAT_ALL = 0x3Fu;   // every material type (1 << SRT_GLOSSY ..
 constexpr uint32_t MAT_BVH = 0x40u;   // a triangle BVH (the traversal code)
 constexpr uint32_t MAT_TRI = 0x80u;   // Triangle colliders intersected one by one (collider loops, tie re-tests)
 constexpr uint32_t MAT_NMAP = 0x100u; // a normal-mapped material (shading_normal's texel path)
+constexpr uint32_t MAT_LDS_STACK = 0x200u;   // the BVH traversal stack's first entries in LDS (256-thread blocks)
+constexpr uint32_t MAT_LDS_NARROW = 0x400u;  // ... in k_frame's 64-thread blocks (half as many entries)
 constexpr uint32_t MAT_GENERIC = MAT_ALL | MAT_TRI | MAT_NMAP;
 constexpr uint32_t mat_bit(int type) { return 1u << type; }
 // Collider sequence known at compile time (bits 12..31 of a variant's feature mask, 0: the scene's
@@ -289,6 +291,10 @@ struct BvhNode {
 static_assert(sizeof(BvhNode) == 128, "one 128-byte line per BVH node");
 constexpr int32_t BVH_EMPTY = (int32_t)0x80000000;
 constexpr int BVH_STACK = 32;  // (3 entries per 4-wide level at most: depth <= 10 levels)
+#ifndef RT_BVH_LDS
+#define RT_BVH_LDS 16  // (-DRT_BVH_LDS=2: a check build whose stacks overflow into the private part)
+#endif
+constexpr int BVH_LDS = RT_BVH_LDS;  // (MAT_LDS_STACK) entries of a thread's stack kept in LDS, the rest private
 
 // The kernel's dynamic LDS: the texture tables [0, nlut_lds) staged by the trace kernels first
 // (rt_kernels.hip stage_luts), read directly (no pointer in the scene view, so the kernels' scene view
@@ -801,6 +807,46 @@ RT_UNROLL
     cs(1, 2);
 }
 
+// A thread's traversal stack: a private array (scratch: its dynamic indexing keeps it out of
+// registers), or (MAT_LDS_STACK) its first NL entries in LDS, column threadIdx.x of an [NL][NT]
+// array (a wave's 64 lanes on consecutive words: conflict-free), the rest private.  Scratch entries
+// go through L1/L2 and, a whole chip of stacks outgrowing them, to HBM, and a pop's latency is on the
+// traversal's critical path: the fused mesh kernel 4.44 -> 3.20 ms per launch, spilled VGPRs 121 -> 29
+// (profiles/r06_bvh_lds_stack_ab.txt).
+constexpr int bvh_lds_entries(uint32_t feat) {
+    return !(feat & MAT_LDS_STACK) ? 0 : (feat & MAT_LDS_NARROW) ? BVH_LDS / 2 : BVH_LDS;
+}
+constexpr int bvh_lds_threads(uint32_t feat) { return (feat & MAT_LDS_NARROW) ? 64 : 256; }
+#if defined(__HIP_DEVICE_COMPILE__)
+template <int NL, int NT>
+__device__ __forceinline__ uint64_t* bvh_lds_column() {
+    __shared__ uint64_t stack_lds[NL * NT];
+    return stack_lds + threadIdx.x;
+}
+#endif
+template <uint32_t FEAT>
+struct BvhStack {
+#if defined(__HIP_DEVICE_COMPILE__)
+    static constexpr int NL = bvh_lds_entries(FEAT), NT = bvh_lds_threads(FEAT);
+    uint64_t* col = NL > 0 ? bvh_lds_column<(NL > 0 ? NL : 1), NT>() : nullptr;
+#else
+    static constexpr int NL = 0, NT = 1;
+#endif
+    uint64_t priv[BVH_STACK - NL];
+    RT_HDM void put(int i, uint64_t e) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (NL > 0 && i < NL) { col[i * NT] = e; return; }
+#endif
+        priv[i - NL] = e;
+    }
+    RT_HDM uint64_t get(int i) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (NL > 0 && i < NL) return col[i * NT];
+#endif
+        return priv[i - NL];
+    }
+};
+
 // Nearest BVH triangle, merged into (best, id, bo, ties) with the reference's rule independent of
 // visiting order: the smallest distance wins, among equal distances the lowest collider index,
 // and `ties` records that another collider hit at that distance.  Boxes entered beyond `best` are
@@ -808,9 +854,10 @@ RT_UNROLL
 // are pushed farthest first (the nearest is popped next) with their entry distance, which prunes them
 // again on pop.  Triangles never return NaN (a NaN ray fails every comparison of triangle_hit and
 // misses).
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH>
 RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, double& bo, bool& ties) {
     const BvhRay R = bvh_ray(S, O, D);
-    uint64_t stack[BVH_STACK];
+    BvhStack<FEAT> stack;
     int sp = 0;
     // the node (or leaf) visited next stays in a register: a node's nearest hit child is taken
     // directly, the others pushed; the stack is read only when a subtree is done
@@ -835,7 +882,7 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
             if (t[0] != INFINITY) {
                 RT_UNROLL
                 for (int k = 3; k >= 1; --k)
-                    if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = bvh_entry(t[k], c[k]);
+                    if (t[k] != INFINITY && sp < BVH_STACK) stack.put(sp++, bvh_entry(t[k], c[k]));
                 code = c[0];
                 continue;
             }
@@ -843,7 +890,7 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
         // pop the nearest pending subtree not entered beyond `best`
         bool more = false;
         while (sp > 0) {
-            const uint64_t e = stack[--sp];
+            const uint64_t e = stack.get(--sp);
             if ((double)bvh_u2f((uint32_t)(e >> 32)) > best) continue;
             code = (int32_t)(uint32_t)e;
             more = true;
@@ -854,9 +901,10 @@ RT_HD void bvh_nearest(const SceneView& S, d3 O, d3 D, double& best, int& id, do
 }
 
 // Any shadowed BVH triangle closer than `stop` along L: returns its distance, else FARAWAY.
+template <uint32_t FEAT = MAT_GENERIC | MAT_BVH>
 RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
     const BvhRay R = bvh_ray(S, O, L);
-    int32_t stack[BVH_STACK];
+    BvhStack<FEAT> stack;
     int sp = 0;
     int32_t code = 0;
     for (;;) {
@@ -876,13 +924,13 @@ RT_HD double bvh_shadow(const SceneView& S, d3 O, d3 L, double stop) {
             if (t[0] != INFINITY) {
                 RT_UNROLL
                 for (int k = 3; k >= 1; --k)
-                    if (t[k] != INFINITY && sp < BVH_STACK) stack[sp++] = c[k];
+                    if (t[k] != INFINITY && sp < BVH_STACK) stack.put(sp++, (uint32_t)c[k]);
                 code = c[0];
                 continue;
             }
         }
         if (sp == 0) break;
-        code = stack[--sp];
+        code = (int32_t)(uint32_t)stack.get(--sp);
     }
     return FARAWAY;
 }
@@ -952,7 +1000,7 @@ RT_HD int nearest_hit(const SceneView& S, d3 O, d3 D, double& tn, double& on, bo
             else if (t == best && id >= 0) ties = true;
         }
     }
-    if (BVH && S.bvh_nodes > 0) bvh_nearest(S, O, D, best, id, bo, ties);
+    if (BVH && S.bvh_nodes > 0) bvh_nearest<FEAT>(S, O, D, best, id, bo, ties);
     if (nan || best == FARAWAY) { tn = nan ? NAN : FARAWAY; on = FARAWAY; ties = false; return -1; }
     tn = best;
     on = bo;
@@ -1066,7 +1114,8 @@ RT_HD double shadow_nearest(const SceneView& S, int light, d3 O, d3 L, double st
             first = false;
         }
     }
-    if (BVH && S.bvh_nodes > 0 && best >= stop) best = np_min(best, bvh_shadow(S, O, L, stop));
+    if (BVH && S.bvh_nodes > 0 && best >= stop)
+        best = np_min(best, bvh_shadow<FEAT>(S, O, L, stop));
     return best;
 }
 

@@ -1129,9 +1129,14 @@ constexpr int OCC = RT_OCC;  // waves/SIMD the trace kernels are built for (regi
 #ifndef RT_FUSE_OCC
 #define RT_FUSE_OCC 3  // waves/SIMD of the fused k_primary (168 VGPRs; its spills: DESIGN.md §3)
 #endif
+#ifndef RT_BVH_LDS_STACK
+#define RT_BVH_LDS_STACK 1  // the BVH variants' traversal stacks start in LDS (rt_device.h BvhStack)
+#endif
+constexpr uint32_t LDS_STK = RT_BVH_LDS_STACK ? MAT_LDS_STACK : 0u, LDS_STK_FRAME = RT_BVH_LDS_STACK ? MAT_LDS_STACK | MAT_LDS_NARROW : 0u;
 #ifndef RT_MESH_FUSE_OCC
 #define RT_MESH_FUSE_OCC RT_FUSE_OCC  // the glossy BVH variant's fused k_primary
 #endif
+constexpr uint32_t MATS_MESH = MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH;  // a glossy TriangleMesh in the ex1 setting
 const Variant VARIANTS[] = {
     {MATS_GLOSSY_SKY, k_primary<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC>, k_frame<MATS_GLOSSY_SKY, OCC>, k_trace<MATS_GLOSSY_SKY, OCC, true>,
      k_primary<MATS_GLOSSY_SKY, RT_FUSE_OCC, true>, k_primary_lean<MATS_GLOSSY_SKY, RT_FUSE_OCC>,
@@ -1141,14 +1146,13 @@ const Variant VARIANTS[] = {
     {MATS_FILM, k_primary<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC>, k_frame<MATS_FILM, OCC>, k_trace<MATS_FILM, OCC, true>},
     {MATS_MC, k_primary<MATS_MC, OCC>, k_trace<MATS_MC, OCC>, k_frame<MATS_MC, OCC>, k_trace<MATS_MC, OCC, true>},
     // a glossy TriangleMesh in the ex1 setting (the mesh bench): the BVH traversal, no other features
-    {MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>,
-     k_frame<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC>, k_trace<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, OCC, true>,
-     k_primary<MATS_GLOSSY_SKY | MAT_TRI | MAT_BVH, RT_MESH_FUSE_OCC, true>},
+    {MATS_MESH, k_primary<MATS_MESH | LDS_STK, OCC>, k_trace<MATS_MESH | LDS_STK, OCC>, k_frame<MATS_MESH | LDS_STK_FRAME, OCC>,
+     k_trace<MATS_MESH | LDS_STK, OCC, true>, k_primary<MATS_MESH | LDS_STK, RT_MESH_FUSE_OCC, true>},
     {MAT_GENERIC, k_primary<MAT_GENERIC, OCC>, k_trace<MAT_GENERIC, OCC>, k_frame<MAT_GENERIC, OCC>,
      k_trace<MAT_GENERIC, OCC, true>},
     // scenes with a triangle BVH (TriangleMesh)
-    {MAT_GENERIC | MAT_BVH, k_primary<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC>,
-     k_frame<MAT_GENERIC | MAT_BVH, OCC>, k_trace<MAT_GENERIC | MAT_BVH, OCC, true>},
+    {MAT_GENERIC | MAT_BVH, k_primary<MAT_GENERIC | MAT_BVH | LDS_STK, OCC>, k_trace<MAT_GENERIC | MAT_BVH | LDS_STK, OCC>,
+     k_frame<MAT_GENERIC | MAT_BVH | LDS_STK_FRAME, OCC>, k_trace<MAT_GENERIC | MAT_BVH | LDS_STK, OCC, true>},
 #endif
 };
 // Variants for scenes of a given collider sequence (rt_device.h seq_of: the colliders intersected in
