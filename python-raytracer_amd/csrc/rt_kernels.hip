@@ -393,6 +393,11 @@ __device__ __forceinline__ void primary_uniforms(const TraceParams& P, int s, ui
 // k_primary's split of primary_uniforms: the pixel-jitter pair (prefetched a sample ahead) and the
 // lens-disk pair (thin-lens cameras only), the same values
 __device__ __forceinline__ void primary_jitter(const TraceParams& P, int s, uint32_t p, uint32_t gpix, double j[2]) {
+#ifdef RT_ABL_JIT  // diagnostic build only: no jitter loads (wrong images; timing only)
+    j[0] = 0.5 + 1e-9 * (double)(s & 7);
+    j[1] = 0.5;
+    return;
+#endif
     if (P.jitter) {
         const int64_t plane = P.jit_plane;
         const double* base = P.jitter + (int64_t)s * 4 * plane + (P.jit_global ? gpix : p);
