@@ -467,7 +467,7 @@ __device__ __forceinline__ void trace_one(const TraceParams& P, Ray& r, bool act
     // added) go through the same waterfall: after shading its collider a tied lane moves on to the
     // next collider (in index order) hit at the same distance, with the next emission round.  One
     // copy of the shaders per kernel (a separate tie loop held a second one: the kernels waited on
-    // instruction fetch ~10 % of their wave cycles, SQ_WAIT_INST_ANY).
+    // ~10 % of their wave cycles in SQ_WAIT_INST_ANY; round 6: issue stalls, the i-cache misses 0.004 %).
     RT_T0(tw0);
     // a SkyBox / Panorama hit without a tie: its texel words fetched now, its colour added after the
     // waterfall of the other colliders (the load latency overlaps their shading; fixed-point sums do
