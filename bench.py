@@ -738,84 +738,98 @@ def main():
 
     # ---- secondary figures --------------------------------------------------------------------
     sec = {}
-    if not args.no_secondary and not args.rgb_to_host and not args.device_outputs and len(rehearse) == 1:
-        # the same frames with the linear RGB copied to host memory as well (rounds 1-4's step)
-        barrier()
-        el2, st2, _ = timed(True)
-        vals2 = (ctypes.c_double * 1)(el2)
-        if world > 1:
-            N.check(lib, lib.srt_comm_allreduce(ctx, vals2, 1, 1))
-        sec["host_rgb"] = {"value": round(total_rays * args.steps / vals2[0] / 1e6, 3),
-                           "ms_per_step": round(vals2[0] / args.steps * 1e3, 4),
-                           "what": "same frames with the linear RGB (f64) copied to pinned host memory as well "
-                                   "(%s)" % ("every rank its rows into the shared host frame, SRT_RENDER_RGB_ROWS"
-                                             if world > 1 else "50 MB per 1080p frame over one PCIe link")}
-    if not args.no_secondary:
-        # one synchronous frame, render() entry -> host memory (latency, not throughput)
-        lat = []
-        stats = []
-        for _ in range(3):
-            s = N.Stats()
-            t1 = time.perf_counter()
-            step(async_ok=False, st=s)
-            lat.append((time.perf_counter() - t1) * 1e3)
-            stats.append(s.as_dict())
-        sec["frame_latency_ms"] = round(float(np.median(lat)), 4)
-        sec["stats"] = stats
-        if stats[0]["kernel_path"] == "fused" and not args.sync:
-            # the pipelined frames' kernel (k_primary_lean, when the scene has one) timed alone in the same
-            # synchronous frames (option sync_lean), for the roofline
-            n0, n1 = ctypes.c_int64(0), ctypes.c_int64(0)
-            N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n0)))
-            N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 1))
-            lean_stats = []
-            try:
-                for _ in range(3):
-                    s = N.Stats()
-                    step(async_ok=False, st=s)
-                    lean_stats.append(s.as_dict())
-            finally:
-                N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 0))
-            N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n1)))
-            if n1.value > n0.value:
-                sec["stats_lean"] = lean_stats
-                # lane utilisation of the pipelined frames' depth loop: one more pipelined frame with the
-                # kernel's counting instantiation (not timed)
-                raw = (ctypes.c_int64 * (2 * 16))()
-                N.check(lib, lib.srt_debug_lane_stats(ctx, 1, None, 0))
-                step()
-                step()
-                N.check(lib, lib.srt_debug_lane_stats(ctx, 0, raw, 16))
-                sec["lane_stats"] = lane_summary([(raw[2 * d] / 2, raw[2 * d + 1] / 2) for d in range(16)])
-        if world == 1 and rows32 is None:
-            # the round-1 headline form: jitter resident in HBM, outputs left in HBM
-            nj = spp * 4 * npix_full
-            jd, od, ud = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
-            N.check(lib, lib.srt_device_alloc(ctx, nj * 8, ctypes.byref(jd)))
-            N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full * 8, ctypes.byref(od)))
-            N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full, ctypes.byref(ud)))
-            np.random.seed(0)
-            jh = np.random.rand(nj)
-            N.check(lib, lib.srt_memcpy(ctx, jd, N.ptr(jh), jh.nbytes))
-            del jh
-            r = N.RenderArgs()
-            r.spp, r.n_rows, r.jitter, r.seed, r.out_rgb, r.out_srgb8 = spp, H, jd, 12345, od, ud
-            r.flags = 0
-            N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(r), None))
-            r.flags = N.RENDER_ASYNC
-            N.check(lib, lib.srt_synchronize(ctx))
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
+
+    def secondaries():
+        if not args.no_secondary and not args.rgb_to_host and not args.device_outputs and len(rehearse) == 1:
+            # the same frames with the linear RGB copied to host memory as well (rounds 1-4's step)
+            barrier()
+            el2, st2, _ = timed(True)
+            vals2 = (ctypes.c_double * 1)(el2)
+            if world > 1:
+                N.check(lib, lib.srt_comm_allreduce(ctx, vals2, 1, 1))
+            sec["host_rgb"] = {"value": round(total_rays * args.steps / vals2[0] / 1e6, 3),
+                               "ms_per_step": round(vals2[0] / args.steps * 1e3, 4),
+                               "what": "same frames with the linear RGB (f64) copied to pinned host memory as well "
+                                       "(%s)" % ("every rank its rows into the shared host frame, SRT_RENDER_RGB_ROWS"
+                                                 if world > 1 else "50 MB per 1080p frame over one PCIe link")}
+        if not args.no_secondary:
+            # one synchronous frame, render() entry -> host memory (latency, not throughput)
+            lat = []
+            stats = []
+            for _ in range(3):
+                s = N.Stats()
+                t1 = time.perf_counter()
+                step(async_ok=False, st=s)
+                lat.append((time.perf_counter() - t1) * 1e3)
+                stats.append(s.as_dict())
+            sec["frame_latency_ms"] = round(float(np.median(lat)), 4)
+            sec["stats"] = stats
+            if stats[0]["kernel_path"] == "fused" and not args.sync:
+                # the pipelined frames' kernel (k_primary_lean, when the scene has one) timed alone in the same
+                # synchronous frames (option sync_lean), for the roofline
+                n0, n1 = ctypes.c_int64(0), ctypes.c_int64(0)
+                N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n0)))
+                N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 1))
+                lean_stats = []
+                try:
+                    for _ in range(3):
+                        s = N.Stats()
+                        step(async_ok=False, st=s)
+                        lean_stats.append(s.as_dict())
+                finally:
+                    N.check(lib, lib.srt_set_option(ctx, b"sync_lean", 0))
+                N.check(lib, lib.srt_debug_lean_launches(ctx, ctypes.byref(n1)))
+                if n1.value > n0.value:
+                    sec["stats_lean"] = lean_stats
+                    # lane utilisation of the pipelined frames' depth loop: one more pipelined frame with the
+                    # kernel's counting instantiation (not timed)
+                    raw = (ctypes.c_int64 * (2 * 16))()
+                    N.check(lib, lib.srt_debug_lane_stats(ctx, 1, None, 0))
+                    step()
+                    step()
+                    N.check(lib, lib.srt_debug_lane_stats(ctx, 0, raw, 16))
+                    sec["lane_stats"] = lane_summary([(raw[2 * d] / 2, raw[2 * d + 1] / 2) for d in range(16)])
+            if world == 1 and rows32 is None:
+                # the round-1 headline form: jitter resident in HBM, outputs left in HBM
+                nj = spp * 4 * npix_full
+                jd, od, ud = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+                N.check(lib, lib.srt_device_alloc(ctx, nj * 8, ctypes.byref(jd)))
+                N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full * 8, ctypes.byref(od)))
+                N.check(lib, lib.srt_device_alloc(ctx, 3 * npix_full, ctypes.byref(ud)))
+                np.random.seed(0)
+                jh = np.random.rand(nj)
+                N.check(lib, lib.srt_memcpy(ctx, jd, N.ptr(jh), jh.nbytes))
+                del jh
+                r = N.RenderArgs()
+                r.spp, r.n_rows, r.jitter, r.seed, r.out_rgb, r.out_srgb8 = spp, H, jd, 12345, od, ud
+                r.flags = 0
                 N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(r), None))
-            s = N.Stats()
-            N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(s)))
-            dt = time.perf_counter() - t1
-            sec["device_resident"] = {
-                "value": round(s.total_rays * args.steps / dt / 1e6, 3), "ms_per_step": round(dt / args.steps * 1e3, 4),
-                "what": "same frames with the jitter pre-resident in HBM (uploaded once) and the outputs left in HBM "
-                        "(the round-1 headline; excludes the in-step jitter generation and the host copies)"}
-            for p in (jd, od, ud):
-                lib.srt_device_free(ctx, p)
+                r.flags = N.RENDER_ASYNC
+                N.check(lib, lib.srt_synchronize(ctx))
+                t1 = time.perf_counter()
+                for _ in range(args.steps):
+                    N.check(lib, lib.srt_render(ctx, ctypes.byref(cd), ctypes.byref(r), None))
+                s = N.Stats()
+                N.check(lib, lib.srt_render_finish(ctx, ctypes.byref(s)))
+                dt = time.perf_counter() - t1
+                sec["device_resident"] = {
+                    "value": round(s.total_rays * args.steps / dt / 1e6, 3), "ms_per_step": round(dt / args.steps * 1e3, 4),
+                    "what": "same frames with the jitter pre-resident in HBM (uploaded once) and the outputs left in HBM "
+                            "(the round-1 headline; excludes the in-step jitter generation and the host copies)"}
+                for p in (jd, od, ud):
+                    lib.srt_device_free(ctx, p)
+
+    if world > 1:
+        # (the N > 1 line must not be lost to a figure beside it: a library error in the secondary
+        # frames -- the host-RGB rows into the shared frame, synchronous sharded frames -- is reported in
+        # the line instead; every rank takes the same branch, so no collective is left waiting)
+        try:
+            secondaries()
+        except (RuntimeError, OSError) as e:
+            sec.clear()
+            sec["error"] = "%s: %s" % (type(e).__name__, e)
+    else:
+        secondaries()
 
     if rank == 0:
         rec = {
@@ -864,6 +878,8 @@ def main():
             rec["rehearsal_order"] = order
         if "host_rgb" in sec:
             rec["host_rgb"] = sec["host_rgb"]
+        if "error" in sec:
+            rec["secondary_error"] = sec["error"]
         if "frame_latency_ms" in sec:
             rec["config"]["frame_latency_ms"] = sec["frame_latency_ms"]
             if "device_resident" in sec:

@@ -234,6 +234,8 @@ class FakeSrt:
         elif a.out_srgb8:
             return self.fail("rank %d passed a uint8 output (only rank 0 receives the gathered frame)" % self.rank)
         if a.flags & N.RENDER_RGB_ROWS:
+            if os.environ.get("FAKE_SRT_FAIL_RGB_ROWS"):  # (injected failure: tests/test_bench_n8.py)
+                return self.fail("injected: RGB_ROWS frame failed")
             if a.out_rgb not in self.registered:
                 return self.fail("RGB_ROWS into memory not registered with srt_host_register")
             self._write_rows(a.out_rgb, self.rank)

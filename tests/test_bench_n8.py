@@ -126,3 +126,36 @@ def test_bench_gpus_8_in_process_group(tmp_path, monkeypatch, capsys):
     assert len(fake.frames) == 2 + 4 + 4 + 3
     rgb_checks = [c for c in fake.log["checks"] if c["frame"] == "rgb_rows"]
     assert len(rgb_checks) == 3 and all(c["tiled_exactly"] for c in rgb_checks)
+
+
+def test_bench_gpus_8_line_survives_a_failed_secondary_figure(tmp_path):
+    """A library error in the secondary frames of the N = 8 run (here every rank's SRT_RENDER_RGB_ROWS
+    frame fails, injected in the stand-in) costs the secondary figures, not the line: rank 0 still
+    prints its one JSON line, with the timed value and the error in `secondary_error`, and every rank
+    exits cleanly (the ranks take the same branch, no collective is left waiting)."""
+    W, H, spp, world = 96, 64, 2, 8
+    argv = ["--gpus", "8", "--steps", "4", "--warmup", "2", "--config", "example1_1080p_d5", "--size", "%dx%d" % (W, H),
+            "--spp", str(spp)]
+    port = str(20000 + (os.getpid() + 7919) % 20000)
+    procs = []
+    for r in range(world):
+        env = _env(WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                   FAKE_SRT_FAIL_RGB_ROWS="1")
+        procs.append(subprocess.Popen([sys.executable, "-c", _boot(tmp_path, W, H, spp, argv)], env=env,
+                                      cwd=str(tmp_path), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=300)
+            outs.append((p.returncode, out, err))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (rc, out, err) in enumerate(outs):
+        assert rc == 0, "rank %d rc %d:\n%s" % (r, rc, err[-3000:])
+    lines = [[json.loads(ln) for ln in out.splitlines() if ln.startswith("{")] for _, out, _ in outs]
+    assert [len(x) for x in lines] == [1] + [0] * (world - 1)
+    rec = lines[0][0]
+    assert rec["n_gpus"] == world and rec["value"] > 0
+    assert "injected" in rec["secondary_error"] and "host_rgb" not in rec
