@@ -825,11 +825,6 @@ __device__ __forceinline__ void lds_put(uint32_t* p, uint32_t v) {
 // cornell 800x800 512 spp 4006 -> 3939 ms, but the thin-film example4 4K 13.95 -> 14.09 ms, so the
 // thin-film variants keep rows (profiles/r06_frame_tile_ab.txt).
 constexpr bool frame_tile_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFILM)) == 0; }
-// k_frame's ring drained newest first (a stack: the chunk taken is the last 64 rays pushed, usually
-// the children of the chunk just traced, still in L2) for the thin-film variants: ex4 4K frame 13.83 ->
-// 13.58 ms; oldest first for the rest (ex3 unchanged, cornell's Diffuse fan-out outgrows a stack's
-// ring: 4.02 -> 5.24 s; profiles/r06_rejected_frame_lifo.txt)
-constexpr bool frame_lifo_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFILM)) != 0; }
 // k_frame's ring split in two halves for the refractive variants without thin films or Diffuse: rays
 // travelling inside a medium (which next hit the body they are in) in one, the rest in the other, so
 // that a chunk of the first shades one collider in one pass of the material waterfall: ex3 1080p d8
@@ -837,6 +832,15 @@ constexpr bool frame_lifo_for(uint32_t mats) { return (mats & mat_bit(SRT_THINFI
 // cornell's Diffuse fan-out overflows half a ring (profiles/r06_frame_split_ab.txt)
 constexpr bool frame_split_for(uint32_t mats) {
     return (mats & mat_bit(SRT_REFRACTIVE)) != 0 && (mats & (mat_bit(SRT_THINFILM) | mat_bit(SRT_DIFFUSE))) == 0;
+}
+// k_frame's rings drained newest first (a stack: the chunk taken is the last 64 rays pushed, usually
+// the children of the chunk just traced, still in L2) for the thin-film variants (ex4 4K frame 13.83 ->
+// 13.58 ms) and the split-ring ones (ex3 1080p d8, same box: frame 2.55-2.58 -> 2.45-2.47 ms,
+// device-resident 2.41-2.43 -> 2.14-2.18 ms, profiles/r06_frame_split_lifo_ab.txt; before the split,
+// one FIFO-or-stack ring gave ex3 no change); oldest first for the rest (cornell's Diffuse fan-out
+// outgrows a stack's ring: 4.02 -> 5.24 s; profiles/r06_rejected_frame_lifo.txt)
+constexpr bool frame_lifo_for(uint32_t mats) {
+    return (mats & mat_bit(SRT_THINFILM)) != 0 || frame_split_for(mats);
 }
 __device__ __forceinline__ uint32_t frame_tile_index(bool tiled, uint32_t d, uint32_t W) {
     if (!tiled) return d;
